@@ -1,0 +1,144 @@
+"""ctypes binding of libpcg.so, the C ABI declared in include/pcg.h.
+
+The HIP extension is mandatory: importing this module raises if libpcg.so is
+missing, and decoding raises if no GPU is present.  There is no CPU fallback.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libpcg.so")
+
+PCG_OK = 0
+PCG_E_ARG = -1
+PCG_E_FROZEN = -2
+PCG_E_HIP = -3
+PCG_E_UNSUPPORTED = -4
+PCG_E_NODEVICE = -5
+
+CRC_KINDS = (0, 8, 16, 32)
+
+
+class PcgError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"pcg error {code}: {msg}")
+        self.code = code
+
+
+class PlanDesc(C.Structure):
+    _fields_ = [
+        ("block_length", C.c_uint32),
+        ("info_length", C.c_uint32),
+        ("list_size", C.c_uint32),
+        ("node_count", C.c_uint32),
+        ("op_count", C.c_uint32),
+        ("lds_bytes", C.c_uint32),
+        ("scratch_bytes", C.c_uint64),
+        ("crc_kind", C.c_int32),
+        ("systematic", C.c_int32),
+    ]
+
+
+_lib = None
+
+
+def _prefer_torch_hip_runtime():
+    """Load PyTorch's bundled HIP runtime first when torch is installed.
+
+    torch ships its own libamdhip64/libhsa-runtime64 (SONAME libamdhip64.so.7) and
+    its libraries bind them as "libamdhip64.so".  If libpcg.so were loaded first,
+    /opt/rocm's runtime would be mapped and torch would then map a second HSA
+    runtime, after which torch sees no GPU.  Loading torch first makes
+    libpcg.so's DT_NEEDED libamdhip64.so.7 resolve to the runtime torch already
+    holds, so device pointers and streams are shared.
+    """
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _prefer_torch_hip_runtime()
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} not found: build the HIP extension first "
+                "(python -c 'import __graft_entry__ as g; g.build()')")
+        L = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        L.pcg_plan_create.argtypes = [C.POINTER(P), C.c_uint32, C.c_uint32, P, C.c_uint32, C.c_int, C.c_int, C.c_int]
+        L.pcg_decode_f32.argtypes = [P, P, C.c_uint64, P, P, P, P]
+        L.pcg_decode_f32_host.argtypes = [P, P, C.c_uint64, P, P, P]
+        L.pcg_plan_describe.argtypes = [P, C.POINTER(PlanDesc)]
+        L.pcg_plan_destroy.argtypes = [P]
+        L.pcg_plan_destroy.restype = None
+        L.pcg_last_error.restype = C.c_char_p
+        L.pcg_device_count.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise PcgError(rc, lib().pcg_last_error().decode(errors="replace"))
+
+
+def device_count():
+    return lib().pcg_device_count()
+
+
+class Plan:
+    """Owns one pcg_plan (decoder tree + device schedule for one device)."""
+
+    def __init__(self, N, L, frozen, systematic=True, crc=8, device=0):
+        fr = np.ascontiguousarray(np.asarray(list(frozen), dtype=np.uint32))
+        h = C.c_void_p()
+        _check(lib().pcg_plan_create(C.byref(h), int(N), int(L), fr.ctypes.data if fr.size else None,
+                                     int(fr.size), int(bool(systematic)), int(crc), int(device)))
+        self._h = h
+        self.N, self.L, self.K = int(N), int(L), int(N) - int(fr.size)
+        self.kb = (self.K + 7) // 8
+        self.device = device
+
+    def describe(self):
+        d = PlanDesc()
+        _check(lib().pcg_plan_describe(self._h, C.byref(d)))
+        return {k: getattr(d, k) for k, _ in PlanDesc._fields_}
+
+    def decode_host(self, llr, want_ok=True, want_metrics=False):
+        llr = np.ascontiguousarray(llr, dtype=np.float32).reshape(-1, self.N)
+        F = llr.shape[0]
+        info = np.zeros((F, self.kb), np.uint8)
+        ok = np.zeros(F, np.uint8) if want_ok else None
+        met = np.zeros((F, self.L), np.float32) if want_metrics else None
+        _check(lib().pcg_decode_f32_host(self._h, llr.ctypes.data, F, info.ctypes.data,
+                                         None if ok is None else ok.ctypes.data,
+                                         None if met is None else met.ctypes.data))
+        return info, ok, met
+
+    def decode_device(self, llr, info, ok=None, metrics=None, stream=None):
+        """Device-resident decode; arguments are torch CUDA tensors (or raw ints)."""
+        def ptr(t):
+            if t is None:
+                return None
+            return t if isinstance(t, int) else t.data_ptr()
+        F = llr.shape[0] if hasattr(llr, "shape") else None
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(llr.device).cuda_stream
+        _check(lib().pcg_decode_f32(self._h, ptr(llr), F, ptr(info), ptr(ok), ptr(metrics), stream))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().pcg_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,302 @@
+// capi.cpp -- the C ABI of include/pcg.h on top of the HIP kernels.
+#include "../../include/pcg.h"
+
+#include "kernels.hpp"
+#include "plan.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+struct pcg_plan {
+    pcg::PlanHost host;
+    int device = 0;
+    uint32_t* d_ops = nullptr;
+    uint16_t* d_info_pos = nullptr;
+    uint32_t* d_crc_m = nullptr;
+    uint32_t wave_lds_floats = 0;
+    uint32_t lds_stage_limit = 0;
+    uint64_t scratch_floats = 0;  // per codeword
+    float* d_scratch = nullptr;   // grown on demand
+    uint64_t scratch_frames = 0;  // capacity in codewords
+    // host-pointer path staging
+    float* d_llr = nullptr;
+    uint8_t* d_info = nullptr;
+    uint8_t* d_ok = nullptr;
+    float* d_met = nullptr;
+    uint64_t stage_frames = 0;
+};
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg)
+{
+    g_last_error = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what)
+{
+    return fail(PCG_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct DeviceGuard {
+    int prev = 0;
+    bool ok = false;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) == hipSuccess && hipSetDevice(dev) == hipSuccess)
+            ok = true;
+    }
+    ~DeviceGuard()
+    {
+        if (ok)
+            (void)hipSetDevice(prev);
+    }
+};
+
+void free_plan_device(pcg_plan* p)
+{
+    (void)hipFree(p->d_ops);
+    (void)hipFree(p->d_info_pos);
+    (void)hipFree(p->d_crc_m);
+    (void)hipFree(p->d_scratch);
+    (void)hipFree(p->d_llr);
+    (void)hipFree(p->d_info);
+    (void)hipFree(p->d_ok);
+    (void)hipFree(p->d_met);
+}
+
+} // namespace
+
+extern "C" {
+
+const char* pcg_last_error(void) { return g_last_error.c_str(); }
+
+int pcg_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess)
+        return 0;
+    return n;
+}
+
+int pcg_plan_create(pcg_plan** out,
+                    uint32_t N,
+                    uint32_t L,
+                    const uint32_t* frozen,
+                    uint32_t n_frozen,
+                    int systematic,
+                    int crc_kind,
+                    int device)
+{
+    if (!out)
+        return fail(PCG_E_ARG, "plan output pointer is null");
+    *out = nullptr;
+    auto* p = new pcg_plan();
+    std::string err;
+    int rc = pcg::build_plan(p->host, N, L, frozen, n_frozen, systematic, crc_kind, &err);
+    if (rc != 0) {
+        delete p;
+        return fail(rc, err);
+    }
+    if (L == 1) {
+        p->wave_lds_floats = pcg::sc_wave_lds_floats(N);
+    } else {
+        rc = pcg::scl_layout(N, L, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats);
+        if (rc != 0) {
+            delete p;
+            return fail(rc, "list decoding layout unsupported for this N/L");
+        }
+    }
+    if (device < 0) { // host-only plan: classification / validation without a GPU
+        p->device = -1;
+        *out = p;
+        return PCG_OK;
+    }
+    int ndev = pcg_device_count();
+    if (ndev <= 0) {
+        delete p;
+        return fail(PCG_E_NODEVICE, "no HIP device available");
+    }
+    if (device >= ndev) {
+        delete p;
+        return fail(PCG_E_ARG, "device index out of range");
+    }
+    p->device = device;
+    DeviceGuard g(device);
+    if (!g.ok) {
+        delete p;
+        return fail(PCG_E_HIP, "hipSetDevice failed");
+    }
+    const auto& h = p->host;
+    hipError_t e;
+    if ((e = hipMalloc(&p->d_ops, 4 * std::max<size_t>(1, h.ops.size()))) != hipSuccess ||
+        (e = hipMalloc(&p->d_info_pos, 2 * std::max<size_t>(1, h.info_pos.size()))) != hipSuccess ||
+        (e = hipMalloc(&p->d_crc_m, 4 * std::max<size_t>(1, h.crc_m.size()))) != hipSuccess) {
+        free_plan_device(p);
+        delete p;
+        return hip_fail(e, "hipMalloc(plan)");
+    }
+    if ((e = hipMemcpy(p->d_ops, h.ops.data(), 4 * h.ops.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+        (!h.info_pos.empty() &&
+         (e = hipMemcpy(p->d_info_pos, h.info_pos.data(), 2 * h.info_pos.size(), hipMemcpyHostToDevice)) !=
+             hipSuccess) ||
+        (!h.crc_m.empty() &&
+         (e = hipMemcpy(p->d_crc_m, h.crc_m.data(), 4 * h.crc_m.size(), hipMemcpyHostToDevice)) != hipSuccess)) {
+        free_plan_device(p);
+        delete p;
+        return hip_fail(e, "hipMemcpy(plan)");
+    }
+    *out = p;
+    return PCG_OK;
+}
+
+int pcg_plan_describe(const pcg_plan* p, pcg_plan_desc* d)
+{
+    if (!p || !d)
+        return fail(PCG_E_ARG, "null argument");
+    d->block_length = p->host.N;
+    d->info_length = p->host.K;
+    d->list_size = p->host.L;
+    d->node_count = p->host.node_count;
+    d->op_count = (uint32_t)p->host.ops.size();
+    d->lds_bytes = p->wave_lds_floats * 4;
+    d->scratch_bytes = p->scratch_floats * 4;
+    d->crc_kind = p->host.crc_kind;
+    d->systematic = p->host.systematic;
+    return PCG_OK;
+}
+
+int pcg_decode_f32(pcg_plan* p,
+                   const float* llr,
+                   uint64_t F,
+                   uint8_t* info,
+                   uint8_t* ok,
+                   float* metrics,
+                   void* stream)
+{
+    if (!p)
+        return fail(PCG_E_ARG, "null plan");
+    if (F == 0)
+        return PCG_OK;
+    if (!llr || !info)
+        return fail(PCG_E_ARG, "null llr/info buffer");
+    if (p->device < 0)
+        return fail(PCG_E_NODEVICE, "host-only plan (created with device < 0)");
+    DeviceGuard g(p->device);
+    const auto& h = p->host;
+    pcg::KernelArgs a{};
+    a.llr = llr;
+    a.F = F;
+    a.ops = p->d_ops;
+    a.nops = (uint32_t)h.ops.size();
+    a.N = h.N;
+    a.log2N = h.log2N;
+    a.K = h.K;
+    a.kb = (h.K + 7) / 8;
+    a.L = h.L;
+    a.info_pos = p->d_info_pos;
+    a.crc_m = p->d_crc_m;
+    a.crc_c0 = h.crc_c0;
+    a.systematic = h.systematic;
+    a.info = info;
+    a.ok = ok;
+    a.metrics = metrics;
+    a.wave_lds_floats = p->wave_lds_floats;
+    a.lds_stage_limit = p->lds_stage_limit;
+    a.scratch_floats = p->scratch_floats;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc;
+    if (h.L == 1) {
+        rc = pcg::launch_sc(a, s);
+    } else {
+        if (p->scratch_floats > 0) {
+            const uint64_t need = pcg::scl_scratch_frames(F);
+            if (need > p->scratch_frames) {
+                (void)hipFree(p->d_scratch);
+                p->d_scratch = nullptr;
+                p->scratch_frames = 0;
+                hipError_t e = hipMalloc(&p->d_scratch, need * p->scratch_floats * sizeof(float));
+                if (e != hipSuccess)
+                    return hip_fail(e, "hipMalloc(scratch)");
+                p->scratch_frames = need;
+            }
+            a.scratch = p->d_scratch;
+        }
+        rc = pcg::launch_scl(a, s);
+    }
+    if (rc != 0)
+        return fail(rc, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    return PCG_OK;
+}
+
+int pcg_decode_f32_host(pcg_plan* p, const float* llr, uint64_t F, uint8_t* info, uint8_t* ok, float* metrics)
+{
+    if (!p)
+        return fail(PCG_E_ARG, "null plan");
+    if (F == 0)
+        return PCG_OK;
+    if (!llr || !info)
+        return fail(PCG_E_ARG, "null llr/info buffer");
+    if (p->device < 0)
+        return fail(PCG_E_NODEVICE, "host-only plan (created with device < 0)");
+    DeviceGuard g(p->device);
+    const auto& h = p->host;
+    const uint64_t kb = (h.K + 7) / 8;
+    const uint64_t chunk = std::min<uint64_t>(F, 1u << 16);
+    hipError_t e;
+    if (p->stage_frames < chunk) {
+        (void)hipFree(p->d_llr);
+        (void)hipFree(p->d_info);
+        (void)hipFree(p->d_ok);
+        (void)hipFree(p->d_met);
+        p->d_llr = nullptr;
+        p->d_info = nullptr;
+        p->d_ok = nullptr;
+        p->d_met = nullptr;
+        p->stage_frames = 0;
+        if ((e = hipMalloc(&p->d_llr, chunk * h.N * sizeof(float))) != hipSuccess ||
+            (e = hipMalloc(&p->d_info, chunk * std::max<uint64_t>(kb, 1))) != hipSuccess ||
+            (e = hipMalloc(&p->d_ok, chunk)) != hipSuccess ||
+            (e = hipMalloc(&p->d_met, chunk * h.L * sizeof(float))) != hipSuccess)
+            return hip_fail(e, "hipMalloc(staging)");
+        p->stage_frames = chunk;
+    }
+    for (uint64_t f0 = 0; f0 < F; f0 += chunk) {
+        const uint64_t n = std::min(chunk, F - f0);
+        if ((e = hipMemcpy(p->d_llr, llr + f0 * h.N, n * h.N * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
+            return hip_fail(e, "hipMemcpy(H2D)");
+        int rc = pcg_decode_f32(p, p->d_llr, n, p->d_info, ok ? p->d_ok : nullptr,
+                                metrics ? p->d_met : nullptr, nullptr);
+        if (rc != 0)
+            return rc;
+        if ((e = hipMemcpy(info + f0 * kb, p->d_info, n * kb, hipMemcpyDeviceToHost)) != hipSuccess)
+            return hip_fail(e, "hipMemcpy(D2H info)");
+        if (ok && (e = hipMemcpy(ok + f0, p->d_ok, n, hipMemcpyDeviceToHost)) != hipSuccess)
+            return hip_fail(e, "hipMemcpy(D2H ok)");
+        if (metrics &&
+            (e = hipMemcpy(metrics + f0 * h.L, p->d_met, n * h.L * sizeof(float), hipMemcpyDeviceToHost)) !=
+                hipSuccess)
+            return hip_fail(e, "hipMemcpy(D2H metrics)");
+    }
+    return PCG_OK;
+}
+
+void pcg_plan_destroy(pcg_plan* p)
+{
+    if (!p)
+        return;
+    if (p->device >= 0) {
+        DeviceGuard g(p->device);
+        free_plan_device(p);
+    }
+    delete p;
+}
+
+} // extern "C"

@@ -1,0 +1,41 @@
+// kernels.hpp -- device launch interface shared by the C ABI and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pcg {
+
+struct KernelArgs {
+    const float* llr;         // F x N channel LLRs (device)
+    uint64_t F;
+    const uint32_t* ops;      // flattened schedule (device)
+    uint32_t nops;
+    uint32_t N, log2N, K, kb, L;
+    const uint16_t* info_pos; // K info positions (device)
+    const uint32_t* crc_m;    // K syndrome columns (device)
+    uint32_t crc_c0;
+    int systematic;
+    uint8_t* info;            // F x kb (device)
+    uint8_t* ok;              // F or null
+    float* metrics;           // F x L or null (SCL)
+    uint32_t wave_lds_floats; // LDS floats per wave (codeword)
+    float* scratch;           // global per-codeword scratch (SCL large stages)
+    uint64_t scratch_floats;  // per codeword
+    uint32_t lds_stage_limit; // SCL: stages < limit live in LDS
+};
+
+// LDS floats one SC codeword needs: alpha (N floats, index 0 unused) + packed bits.
+inline uint32_t sc_wave_lds_floats(uint32_t N) { return N + (N >= 64 ? N / 32 : 2) + 2; }
+
+int launch_sc(const KernelArgs& a, hipStream_t stream);
+int launch_scl(const KernelArgs& a, hipStream_t stream);
+
+} // namespace pcg
+
+namespace pcg {
+// SCL LDS / scratch layout for (N, L): returns 0 or PCG_E_UNSUPPORTED.
+int scl_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* lds_stage_limit,
+               uint64_t* scratch_floats);
+// codewords that need scratch at once for a launch of F frames
+uint64_t scl_scratch_frames(uint64_t F);
+} // namespace pcg

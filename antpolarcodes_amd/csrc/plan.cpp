@@ -1,0 +1,245 @@
+// plan.cpp -- build the flattened decoder schedule (see plan.hpp).
+#include "plan.hpp"
+
+#include "crc_host.hpp"
+
+#include <random>
+
+namespace pcg {
+
+namespace {
+
+struct Err {
+    int code;
+    std::string msg;
+};
+
+void split(const std::vector<uint32_t>& f,
+           uint32_t half,
+           std::vector<uint32_t>& l,
+           std::vector<uint32_t>& r)
+{
+    l.clear();
+    r.clear();
+    for (uint32_t v : f) {
+        if (v < half)
+            l.push_back(v);
+        else
+            r.push_back(v - half);
+    }
+}
+
+uint32_t ilog2(uint32_t n) { return (uint32_t)__builtin_ctz(n); }
+
+uint32_t mkop(uint32_t code, uint32_t n, uint32_t off)
+{
+    return code | (ilog2(n) << 8) | (off << 16);
+}
+
+std::string fmt_frozen(const std::vector<uint32_t>& f)
+{
+    std::string s = "[";
+    for (size_t i = 0; i < f.size(); ++i) {
+        if (i)
+            s += ", ";
+        s += std::to_string(f[i]);
+    }
+    return s + "]";
+}
+
+// FastSscAvx::createDecoder (fastssc_avx_float.cpp:797-896), emitted in decode order:
+//   RateR : F, <left>, G, <right>, COMB        (RateRNode::decode :148-155; ShortRateRNode
+//           :178-185 has the same observable semantics on packed sign bits)
+//   ROne  : F, <left>, RONE                    (:198-219)
+//   ZeroR : G0, <right>, COPY0                 (:232-237)
+void sc_emit(PlanHost& p, const std::vector<uint32_t>& f, uint32_t n, uint32_t off)
+{
+    const uint32_t nf = (uint32_t)f.size();
+    p.node_count++;
+    auto leaf = [&](uint32_t code) {
+        p.node_types.push_back((int)code);
+        p.ops.push_back(mkop(code, n, off));
+    };
+    if (nf == n) return leaf(OP_L_R0);
+    if (nf == 0) return leaf(OP_L_R1);
+    if (nf == n - 1) return leaf(OP_L_REP);
+    if (nf == 1) return leaf(OP_L_SPC);
+    if (nf == n - 2) {
+        for (uint32_t i = 0; i < nf; ++i)
+            if (f[i] != i)
+                throw Err{ -2, fmt_frozen(f) };
+        if (n < 4)
+            throw Err{ -2, "Minimum block length for double Repetition code is 4!" };
+        return leaf(OP_L_DREP);
+    }
+    if (nf == 2 && f[0] == 0 && f[1] == 1)
+        return leaf(n == 8 ? OP_L_DSPC8 : OP_L_DSPC);
+    if (nf == n - 3 && n > 8 && f[nf - 1] == n - 4) {
+        for (uint32_t i = 0; i < nf; ++i)
+            if (f[i] != i)
+                throw Err{ -2, fmt_frozen(f) };
+        return leaf(OP_L_TREP);
+    }
+    if (nf == n - 4 && f[nf - 1] == n - 4 && f[nf - 2] == n - 6)
+        return leaf(OP_L_TYPE5);
+    if (n == 8 && nf == 3 && f[0] == 0 && f[1] == 1 && f[2] == 2)
+        return leaf(OP_L_REPR1);
+    if (n == 8 && nf == 5 && f[nf - 1] == n - 4 && f[nf - 2] == n - 5)
+        return leaf(OP_L_ZSPC8);
+
+    const uint32_t h = n / 2;
+    std::vector<uint32_t> lf, rf;
+    split(f, h, lf, rf);
+    p.node_types.push_back(0);
+    if (n <= 8) { // ShortRateRNode
+        p.ops.push_back(mkop(OP_F, n, off));
+        sc_emit(p, lf, h, off);
+        p.ops.push_back(mkop(OP_G, n, off));
+        sc_emit(p, rf, h, off + h);
+        p.ops.push_back(mkop(OP_COMB, n, off));
+        return;
+    }
+    if (lf.size() == h && rf.size() == 1) { // ZeroSpcDecoder (a leaf kind)
+        p.node_types.back() = OP_L_ZSPC;
+        p.ops.push_back(mkop(OP_L_ZSPC, n, off));
+        return;
+    }
+    if (rf.empty()) { // ROneNode: the right child is an unused dummy Node
+        p.ops.push_back(mkop(OP_F, n, off));
+        sc_emit(p, lf, h, off);
+        p.ops.push_back(mkop(OP_RONE, n, off));
+        return;
+    }
+    if (lf.size() == h) { // ZeroRNode: the left child is an unused dummy Node
+        p.ops.push_back(mkop(OP_G0, n, off));
+        sc_emit(p, rf, h, off + h);
+        p.ops.push_back(mkop(OP_COPY0, n, off));
+        return;
+    }
+    p.ops.push_back(mkop(OP_F, n, off));
+    sc_emit(p, lf, h, off);
+    p.ops.push_back(mkop(OP_G, n, off));
+    sc_emit(p, rf, h, off + h);
+    p.ops.push_back(mkop(OP_COMB, n, off));
+}
+
+// SclAvx::createDecoder (scl_avx_float.cpp:624-651), RateRNode::decode order (:229-263).
+void scl_emit(PlanHost& p, const std::vector<uint32_t>& f, uint32_t n, uint32_t off)
+{
+    const uint32_t nf = (uint32_t)f.size();
+    p.node_count++;
+    auto leaf = [&](uint32_t code) {
+        p.node_types.push_back((int)code);
+        p.ops.push_back(mkop(code, n, off));
+    };
+    if (nf == 0) return leaf(OP_S_R1);
+    if (nf == n) return leaf(OP_S_R0);
+    if (nf == n - 1 && n < 8) return leaf(OP_S_REP);
+    if (nf == 1) return leaf(OP_S_SPC);
+    const uint32_t h = n / 2;
+    std::vector<uint32_t> lf, rf;
+    split(f, h, lf, rf);
+    p.node_types.push_back(0);
+    p.ops.push_back(mkop(OP_F, n, off));
+    scl_emit(p, lf, h, off);
+    p.ops.push_back(mkop(OP_G, n, off));
+    scl_emit(p, rf, h, off + h);
+    p.ops.push_back(mkop(OP_COMB, n, off));
+}
+
+} // namespace
+
+int build_plan(PlanHost& p,
+               uint32_t N,
+               uint32_t L,
+               const uint32_t* frozen,
+               uint32_t nf,
+               int systematic,
+               int crc_kind,
+               std::string* err)
+{
+    p = PlanHost();
+    if (N < 8 || N > 32768 || (N & (N - 1))) {
+        *err = "block length must be a power of two in [8, 32768]";
+        return -1;
+    }
+    if (L < 1 || L > 32) {
+        *err = "list size must be in [1, 32]";
+        return -1;
+    }
+    if (nf > N || (nf > 0 && frozen == nullptr)) {
+        *err = "bad frozen-bit count";
+        return -1;
+    }
+    for (uint32_t i = 0; i < nf; ++i) {
+        if (frozen[i] >= N || (i > 0 && frozen[i] <= frozen[i - 1])) {
+            *err = "frozen bits must be strictly ascending indices < N";
+            return -1;
+        }
+    }
+    if (crc_kind != 0 && crc_kind != 8 && crc_kind != 16 && crc_kind != 32) {
+        *err = "CRC INVALID SIZE!"; // errordetector.cpp:33-35
+        return -1;
+    }
+    p.N = N;
+    p.L = L;
+    p.log2N = ilog2(N);
+    p.K = N - nf;
+    p.systematic = systematic ? 1 : 0;
+    p.crc_kind = crc_kind;
+    p.frozen.assign(frozen, frozen + nf);
+    try {
+        if (L == 1)
+            sc_emit(p, p.frozen, N, 0);
+        else
+            scl_emit(p, p.frozen, N, 0);
+    } catch (Err& e) {
+        *err = e.msg;
+        return e.code;
+    }
+
+    // information-bit LUT (BitContainer::calculateLUT, bitcontainer.cpp:68-84)
+    std::vector<uint8_t> isf(N, 0);
+    for (uint32_t v : p.frozen)
+        isf[v] = 1;
+    for (uint32_t i = 0; i < N; ++i)
+        if (!isf[i])
+            p.info_pos.push_back((uint16_t)i);
+
+    // Affine GF(2) syndrome of the detector over the K info bits, packed MSB-first
+    // into ceil(K/8) bytes exactly as getPackedInformationBits lays them out:
+    //   syndrome(b) = c0 ^ XOR_{j: b_j = 1} m_j ;  check() passes <=> syndrome == 0.
+    const uint32_t K = p.K, kb = (K + 7) / 8;
+    std::vector<uint8_t> msg(kb + 4, 0);
+    uint32_t s0 = 0;
+    crc_syndrome(crc_kind, msg.data(), (int)kb, &s0);
+    p.crc_c0 = s0;
+    p.crc_m.assign(K, 0);
+    for (uint32_t j = 0; j < K; ++j) {
+        std::fill(msg.begin(), msg.end(), 0);
+        msg[j / 8] = (uint8_t)(0x80u >> (j % 8));
+        uint32_t s = 0;
+        crc_syndrome(crc_kind, msg.data(), (int)kb, &s);
+        p.crc_m[j] = s ^ s0;
+    }
+    // self-check of the affine model on random messages
+    std::mt19937 rng(12345);
+    for (int t = 0; t < 8 && K > 0; ++t) {
+        uint32_t acc = s0;
+        std::fill(msg.begin(), msg.end(), 0);
+        for (uint32_t j = 0; j < K; ++j)
+            if (rng() & 1) {
+                msg[j / 8] |= (uint8_t)(0x80u >> (j % 8));
+                acc ^= p.crc_m[j];
+            }
+        uint32_t s = 0;
+        crc_syndrome(crc_kind, msg.data(), (int)kb, &s);
+        if (s != acc) {
+            *err = "internal: detector is not affine over GF(2)";
+            return -4;
+        }
+    }
+    return 0;
+}
+
+} // namespace pcg

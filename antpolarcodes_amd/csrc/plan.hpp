@@ -1,0 +1,78 @@
+// plan.hpp -- decoder plan: the reference's decoder tree, classified exactly as the
+// reference does, flattened into a wave-uniform op schedule for the HIP kernels.
+//
+// Fast-SSC classification : FastSscAvx::createDecoder, fastssc_avx_float.cpp:797-896
+// SCL classification      : SclAvx::createDecoder,     scl_avx_float.cpp:624-651
+// frozen-set split        : splitFrozenBits,           src/polarcode/polarcode.cpp:14-34
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define PCG_HD __host__ __device__
+#else
+#define PCG_HD
+#endif
+
+namespace pcg {
+
+// One op = one 32-bit word: code | stage << 8 | offset << 16.
+//   stage  = log2 of the node size n (the op reads alpha[stage], for F/G writes
+//            alpha[stage-1]);  offset = first codeword-bit position of the node.
+enum OpCode : uint32_t {
+    // internal-node ops (Fast-SSC and SCL)
+    OP_F = 1,     // alpha[s-1][i] = f(alpha[s][i], alpha[s][i+h])            avx_float.h:101-127
+    OP_G = 2,     // alpha[s-1][i] = g(alpha[s][i], alpha[s][i+h], bit[o+i])  avx_float.h:147-164
+    OP_G0 = 3,    // alpha[s-1][i] = alpha[s][i] + alpha[s][i+h]   (ZeroRNode) avx_float.h:166-175
+    OP_COMB = 4,  // bit[o+i] ^= bit[o+h+i]                                    avx_float.h:188-197
+    OP_COPY0 = 5, // bit[o+i]  = bit[o+h+i]                        (ZeroRNode) avx_float.h:199-204
+    OP_RONE = 6,  // fused right rate-1 of ROneNode             fastssc_avx_float.cpp:205-219
+    // Fast-SSC leaves (fastssc_avx_float.cpp)
+    OP_L_R0 = 16,    // :247
+    OP_L_R1 = 17,    // :257-263
+    OP_L_REP = 18,   // :273-287
+    OP_L_SPC = 19,   // :342-373
+    OP_L_DREP = 20,  // :303-332
+    OP_L_DSPC = 21,  // :425-466
+    OP_L_DSPC8 = 22, // :473-488
+    OP_L_TREP = 23,  // :572-589
+    OP_L_TYPE5 = 24, // :762-792
+    OP_L_REPR1 = 25, // :718-739
+    OP_L_ZSPC8 = 26, // :556-565
+    OP_L_ZSPC = 27,  // :503-546 (reproduces the reference's right-half output, Q1)
+    // SCL leaves (scl_avx_float.cpp)
+    OP_S_R0 = 40,  // :316-337
+    OP_S_R1 = 41,  // :353-413
+    OP_S_REP = 42, // :428-481
+    OP_S_SPC = 43, // :498-621
+};
+
+PCG_HD inline uint32_t op_code(uint32_t w) { return w & 0xffu; }
+PCG_HD inline uint32_t op_stage(uint32_t w) { return (w >> 8) & 0xffu; }
+PCG_HD inline uint32_t op_off(uint32_t w) { return w >> 16; }
+
+struct PlanHost {
+    uint32_t N = 0, K = 0, L = 1, log2N = 0;
+    int systematic = 1;
+    int crc_kind = 0;
+    std::vector<uint32_t> frozen;
+    std::vector<uint32_t> ops;      // flattened schedule
+    std::vector<uint16_t> info_pos; // K non-frozen positions, ascending (bitcontainer.cpp:68-84)
+    std::vector<uint32_t> crc_m;    // K affine syndrome columns
+    uint32_t crc_c0 = 0;            // syndrome of the all-zero message
+    uint32_t node_count = 0;
+    std::vector<int> node_types;    // pre-order census (op code of each node; 0 = internal)
+};
+
+// Returns 0, or a negative pcg.h error code with *err set.
+int build_plan(PlanHost& p,
+               uint32_t N,
+               uint32_t L,
+               const uint32_t* frozen,
+               uint32_t nf,
+               int systematic,
+               int crc_kind,
+               std::string* err);
+
+} // namespace pcg

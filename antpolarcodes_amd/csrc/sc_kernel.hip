@@ -1,0 +1,433 @@
+// sc_kernel.hip -- batched Fast-SSC ("SC") polar decoding on CDNA4 (gfx950).
+//
+// One codeword per wavefront.  The wave walks the plan's flattened op schedule
+// (plan.hpp) -- the reference's recursive FastSscAvx node tree
+// (src/polarcode/decoding/fastssc_avx_float.cpp) in decode order -- with every
+// branch wave-uniform.  Per wave, LDS holds the LLR stage buffers alpha[s]
+// (2^s floats at float offset 2^s, s < log2 N; the root stage is the channel
+// LLR frame, read straight from HBM) and the codeword estimate as packed sign
+// bits (N bits).  Only sign bits of the reference's float "bits" are observable
+// (F/G use signs, Combine XORs whole words, the output packs sign bits), so the
+// packed form is exact.  Every arithmetic step reproduces the AVX2 reference's
+// lane order and sign-of-zero behaviour (see oracle/polar_oracle.c).
+#include "plan.hpp"
+#include "kernels.hpp"
+#include "wave.hpp"
+
+namespace pcg {
+
+namespace {
+
+constexpr float FLT_MAX_ = 3.40282347e+38f;
+
+// fill positions [o, o+n) with one bit value
+PCG_DEV void fill_bits(uint32_t* w, uint32_t o, uint32_t n, uint32_t bit, uint32_t lane)
+{
+    if (n >= 32) {
+        const uint32_t v = bit ? 0xffffffffu : 0u;
+        for (uint32_t i = lane; i < n / 32; i += 64)
+            w[(o >> 5) + i] = v;
+    } else if (lane == 0) {
+        const uint32_t sh = o & 31, msk = ((1u << n) - 1u) << sh;
+        w[o >> 5] = (w[o >> 5] & ~msk) | (bit ? msk : 0u);
+    }
+}
+
+// positions [o, o+n) get bit pattern[(i) % period] (period 2, 4 or 8); `pat` bit k = value k
+PCG_DEV void fill_pattern(uint32_t* w, uint32_t o, uint32_t n, uint32_t pat, uint32_t period, uint32_t lane)
+{
+    uint32_t word = 0;
+    for (uint32_t k = 0; k < 32; ++k)
+        word |= ((pat >> (k % period)) & 1u) << k;
+    if (n >= 32) {
+        for (uint32_t i = lane; i < n / 32; i += 64)
+            w[(o >> 5) + i] = word;
+    } else if (lane == 0) {
+        const uint32_t sh = o & 31, msk = ((1u << n) - 1u) << sh;
+        w[o >> 5] = (w[o >> 5] & ~msk) | ((word << sh) & msk);
+    }
+}
+
+// 8 lane partial sums of the reference (each lane from +0.0, chunks ascending,
+// n < 8 padded with +0.0): valid in lanes 0..7.
+template <typename Src>
+PCG_DEV float lane_sum8(Src x, uint32_t n, uint32_t lane)
+{
+    float acc = 0.0f;
+    if (lane < 8) {
+        if (n < 8) {
+            acc = acc + (lane < n ? x[lane] : 0.0f);
+        } else {
+            for (uint32_t i = lane; i < n; i += 8)
+                acc = acc + x[i];
+        }
+    }
+    return acc;
+}
+
+// reduce_add_ps: ((((((s0+s1)+s2)+s3)+s4)+s5)+s6)+s7   avxconvenience.h:256-272
+PCG_DEV float reduce_add8(float s)
+{
+    float r = shfl(s, 0);
+    for (int j = 1; j < 8; ++j)
+        r = r + shfl(s, j);
+    return r;
+}
+
+// _mm256_spc_right4_ps (avx_float.h:289-302) on v held in lanes 0..3 (also valid
+// in any lane k: result for index k&3).  Returns the output sign bit for k&3.
+PCG_DEV uint32_t spc4_sign(float v, uint32_t lane)
+{
+    const uint32_t k = lane & 3;
+    const float v0 = shfl(v, 0), v1 = shfl(v, 1), v2 = shfl(v, 2), v3 = shfl(v, 3);
+    const float m = minps(minps(fabs_(v0), fabs_(v2)), minps(fabs_(v1), fabs_(v3)));
+    const uint32_t par = (fbits(v0) ^ fbits(v1) ^ fbits(v2) ^ fbits(v3)) & 0x80000000u;
+    const float vk = k == 0 ? v0 : k == 1 ? v1 : k == 2 ? v2 : v3;
+    return (sgn(vk) ^ (fabs_(vk) == m ? par : 0u)) >> 31;
+}
+
+template <typename Src>
+PCG_DEV void sc_leaf(uint32_t code, Src x, uint32_t n, uint32_t o, uint32_t* bits, uint32_t lane)
+{
+    switch (code) {
+    case OP_L_R0: // RateZeroDecoder: +INF bits
+        fill_bits(bits, o, n, 0u, lane);
+        break;
+    case OP_L_R1: // RateOneDecoder: bits = LLR
+        for (uint32_t b = 0; b < n; b += 64) {
+            const uint32_t i = b + lane;
+            put_bits(bits, o + b, n < 64 ? n : 64, i < n && (sgn(x[i]) != 0));
+        }
+        break;
+    case OP_L_REP: { // RepetitionDecoder :273-287
+        const float S = reduce_add8(lane_sum8(x, n, lane));
+        fill_bits(bits, o, n, sgn(S) >> 31, lane);
+        break;
+    }
+    case OP_L_DREP: { // DoubleRepetitionDecoder :303-332
+        const float s = lane_sum8(x, n, lane);
+        float ev, od;
+        const float s0 = shfl(s, 0), s1 = shfl(s, 1), s2 = shfl(s, 2), s3 = shfl(s, 3);
+        const float s4 = shfl(s, 4), s5 = shfl(s, 5), s6 = shfl(s, 6), s7 = shfl(s, 7);
+        if (n >= 8) {
+            ev = (s0 + s4) + (s2 + s6);
+            od = (s1 + s5) + (s3 + s7);
+        } else {
+            ev = ((s0 + s2) + s4) + s6;
+            od = ((s1 + s3) + s5) + s7;
+        }
+        fill_pattern(bits, o, n, (sgn(ev) >> 31) | ((sgn(od) >> 31) << 1), 2, lane);
+        break;
+    }
+    case OP_L_SPC: { // SpcDecoder :342-373 (n < 8 padded with +INF)
+        float mv = __builtin_inff();
+        uint32_t mi = 0xffffffffu, par = 0;
+        for (uint32_t i = lane; i < n; i += 64) {
+            const float v = x[i];
+            par ^= fbits(v);
+            const float a = fabs_(v);
+            if (a < mv) {
+                mv = a;
+                mi = i;
+            }
+        }
+        wave_argmin(mv, mi);
+        par = wave_xor(par) & 0x80000000u;
+        if (mi == 0xffffffffu)
+            mi = 0;
+        for (uint32_t b = 0; b < n; b += 64) {
+            const uint32_t i = b + lane;
+            uint32_t s = i < n ? sgn(x[i]) : 0u;
+            if (i == mi)
+                s ^= par;
+            put_bits(bits, o + b, n < 64 ? n : 64, s != 0);
+        }
+        break;
+    }
+    case OP_L_DSPC: { // DoubleSpcDecoder :425-466 (n >= 16)
+        float mv = FLT_MAX_;
+        uint32_t mi = 0, par = 0;
+        if (lane < 8) {
+            for (uint32_t i = lane; i < n; i += 8) {
+                const float v = x[i];
+                par ^= fbits(v);
+                const float a = fabs_(v);
+                if (!(a > mv)) { // _mm256_cmplt_ps is a GT compare: ties -> later index
+                    mv = a;
+                    mi = i;
+                }
+            }
+        }
+        float m[8];
+        uint32_t id[8];
+        uint32_t pe = 0, po = 0;
+        for (int j = 0; j < 8; ++j) {
+            m[j] = shfl(mv, j);
+            id[j] = shfl(mi, j);
+            const uint32_t p = shfl(par, j);
+            if (j & 1)
+                po ^= p;
+            else
+                pe ^= p;
+        }
+        const float ce = minps(minps(m[0], m[4]), minps(m[2], m[6]));
+        const float co = minps(minps(m[1], m[5]), minps(m[3], m[7]));
+        uint32_t ei = 0, oi = 0;
+        for (int j = 6; j >= 0; j -= 2)
+            if (m[j] == ce)
+                ei = id[j];
+        for (int j = 7; j >= 1; j -= 2)
+            if (m[j] == co)
+                oi = id[j];
+        pe &= 0x80000000u;
+        po &= 0x80000000u;
+        for (uint32_t b = 0; b < n; b += 64) {
+            const uint32_t i = b + lane;
+            uint32_t s = i < n ? sgn(x[i]) : 0u;
+            if (i == ei)
+                s ^= pe;
+            if (i == oi)
+                s ^= po;
+            put_bits(bits, o + b, n < 64 ? n : 64, s != 0);
+        }
+        break;
+    }
+    case OP_L_DSPC8: { // DoubleSpcDecoderShort8 :473-488 (multi-flip on ties)
+        const float v = lane < 8 ? x[lane] : 0.0f;
+        float a[8];
+        uint32_t pe = 0, po = 0;
+        for (int j = 0; j < 8; ++j) {
+            const float vj = shfl(v, j);
+            a[j] = fabs_(vj);
+            if (j & 1)
+                po ^= fbits(vj);
+            else
+                pe ^= fbits(vj);
+        }
+        const float ce = minps(minps(a[0], a[4]), minps(a[2], a[6]));
+        const float co = minps(minps(a[1], a[5]), minps(a[3], a[7]));
+        const bool odd = lane & 1;
+        const uint32_t s = sgn(v) ^ ((fabs_(v) == (odd ? co : ce)) ? ((odd ? po : pe) & 0x80000000u) : 0u);
+        put_bits(bits, o, 8, lane < 8 && s != 0);
+        break;
+    }
+    case OP_L_ZSPC8: { // ZeroSpcDecoderShort8 :556-565
+        const uint32_t k = lane & 3;
+        const float v = x[k] + x[k + 4];
+        const uint32_t b = spc4_sign(v, lane);
+        put_bits(bits, o, 8, lane < 8 && b != 0);
+        break;
+    }
+    case OP_L_TREP: { // TripleRepetitionDecoder :572-589
+        const float sl = lane_sum8(x, n, lane);
+        const float v = shfl(sl, lane & 3) + shfl(sl, (lane & 3) + 4);
+        const uint32_t ob = spc4_sign(v, lane);
+        uint32_t pat = 0;
+        for (uint32_t k = 0; k < 4; ++k)
+            pat |= (uint32_t)__builtin_amdgcn_readlane((int)ob, (int)k) << k;
+        fill_pattern(bits, o, n, pat, 4, lane);
+        break;
+    }
+    case OP_L_TYPE5:   // TypeFiveDecoder :762-792
+    case OP_L_REPR1: { // RepetitionRateOneDecoderShort8 :718-739
+        const float l = (code == OP_L_TYPE5) ? lane_sum8(x, n, lane) : (lane < 8 ? x[lane] : 0.0f);
+        const uint32_t k = lane & 3;
+        const float lk = shfl(l, k), lk4 = shfl(l, k + 4);
+        const float r = polar_f(lk, lk4);
+        const float R = (shfl(r, 0) + shfl(r, 1)) + (shfl(r, 2) + shfl(r, 3));
+        const float g = polar_g(lk, lk4, sgn(R));
+        uint32_t ob;
+        if (code == OP_L_TYPE5)
+            ob = spc4_sign(g, lane);
+        else
+            ob = sgn(g) >> 31;
+        uint32_t pat = 0;
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t oq = (uint32_t)__builtin_amdgcn_readlane((int)ob, (int)q);
+            pat |= (oq ^ (sgn(R) >> 31)) << q;
+            pat |= oq << (q + 4);
+        }
+        fill_pattern(bits, o, n, pat, 8, lane);
+        break;
+    }
+    case OP_L_ZSPC: { // ZeroSpcDecoder :503-546 -- right half to both halves (Q1)
+        const uint32_t h = n / 2;
+        float mv = __builtin_inff();
+        uint32_t mi = 0xffffffffu, par = 0;
+        for (uint32_t i = lane; i < h; i += 64) {
+            const float l = x[i] + x[h + i];
+            par ^= fbits(l);
+            const float a = fabs_(l);
+            if (a < mv) {
+                mv = a;
+                mi = i;
+            }
+        }
+        wave_argmin(mv, mi);
+        par = wave_xor(par) & 0x80000000u;
+        if (mi == 0xffffffffu)
+            mi = 0;
+        for (uint32_t b = 0; b < h; b += 64) {
+            const uint32_t i = b + lane;
+            uint32_t s = i < h ? sgn(x[h + i]) : 0u;
+            if (i == mi)
+                s ^= par;
+            const uint32_t c = h < 64 ? h : 64;
+            put_bits(bits, o + b, c, s != 0);
+            put_bits(bits, o + h + b, c, s != 0);
+        }
+        break;
+    }
+    default:
+        break;
+    }
+}
+
+// internal-node ops reading alpha[s] from `x` (LDS stage buffer or the frame in HBM)
+template <typename Src>
+PCG_DEV void sc_inner(uint32_t code, Src x, uint32_t s, uint32_t o, float* alpha, uint32_t* bits, uint32_t lane)
+{
+    const uint32_t h = 1u << (s - 1);
+    float* out = alpha + h;
+    switch (code) {
+    case OP_F:
+        for (uint32_t i = lane; i < h; i += 64)
+            out[i] = polar_f(x[i], x[i + h]);
+        break;
+    case OP_G:
+        for (uint32_t i = lane; i < h; i += 64)
+            out[i] = polar_g(x[i], x[i + h], get_bit(bits, o + i) << 31);
+        break;
+    case OP_G0:
+        for (uint32_t i = lane; i < h; i += 64)
+            out[i] = x[i] + x[i + h];
+        break;
+    case OP_RONE: // ROneNode::rightDecode :205-219
+        for (uint32_t b = 0; b < h; b += 64) {
+            const uint32_t i = b + lane;
+            uint32_t lb = 0, rs = 0;
+            if (i < h) {
+                lb = get_bit(bits, o + i);
+                const float r = polar_g(x[i], x[i + h], lb << 31);
+                rs = sgn(r) >> 31;
+            }
+            const uint32_t c = h < 64 ? h : 64;
+            put_bits(bits, o + b, c, (lb ^ rs) != 0);
+            put_bits(bits, o + h + b, c, rs != 0);
+        }
+        break;
+    default:
+        break;
+    }
+}
+
+PCG_DEV void sc_bits_op(uint32_t code, uint32_t s, uint32_t o, uint32_t* bits, uint32_t lane)
+{
+    const uint32_t h = 1u << (s - 1);
+    if (h >= 32) {
+        const uint32_t wl = o >> 5, wr = (o + h) >> 5;
+        for (uint32_t i = lane; i < h / 32; i += 64)
+            bits[wl + i] = (code == OP_COMB) ? (bits[wl + i] ^ bits[wr + i]) : bits[wr + i];
+    } else if (lane == 0) {
+        const uint32_t sh = o & 31, msk = ((1u << h) - 1u) << sh;
+        const uint32_t w = bits[o >> 5];
+        const uint32_t r = (w >> h) & msk;
+        bits[o >> 5] = (code == OP_COMB) ? (w ^ r) : ((w & ~msk) | r);
+    }
+}
+
+} // namespace
+
+// Non-systematic re-encode in place: x -> u = x G_N on the packed bits
+// (ButterflyFipPacked transform, butterfly_fip.cpp:15-63).  Shared with SCL.
+PCG_DEV void polar_transform_bits(uint32_t* bits, uint32_t N, uint32_t lane)
+{
+    const uint32_t W = N >= 32 ? N / 32 : 1;
+    const uint32_t M[5] = { 0x55555555u, 0x33333333u, 0x0F0F0F0Fu, 0x00FF00FFu, 0x0000FFFFu };
+    for (uint32_t i = lane; i < W; i += 64) {
+        uint32_t w = bits[i];
+        for (uint32_t k = 0, B = 1; k < 5 && B < N; ++k, B <<= 1)
+            w ^= (w >> B) & M[k];
+        bits[i] = w;
+    }
+    wsync();
+    for (uint32_t d = 1; d < W; d <<= 1) {
+        for (uint32_t i = lane; i < W; i += 64)
+            if (!(i & d))
+                bits[i] ^= bits[i + d];
+        wsync();
+    }
+}
+
+// Gather the info bits MSB-first (getPackedInformationBits, bitcontainer.cpp:225-292),
+// optionally store them, and return the detector syndrome (0 <=> check() passes).
+PCG_DEV uint32_t emit_info(const uint32_t* bits, const KernelArgs& a, uint64_t frame, uint32_t lane, bool write)
+{
+    uint32_t syn = 0;
+    for (uint32_t b = lane; b < a.kb; b += 64) {
+        uint32_t byte = 0;
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t idx = 8 * b + j;
+            if (idx < a.K) {
+                const uint32_t bit = get_bit(bits, a.info_pos[idx]);
+                byte |= bit << (7 - j);
+                if (bit)
+                    syn ^= a.crc_m[idx];
+            }
+        }
+        if (write)
+            a.info[frame * a.kb + b] = (uint8_t)byte;
+    }
+    return wave_xor(syn) ^ a.crc_c0;
+}
+
+template <int WAVES>
+__global__ void __launch_bounds__(64 * WAVES) sc_kernel(KernelArgs a)
+{
+    extern __shared__ float smem[];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t frame = (uint64_t)blockIdx.x * WAVES + wv;
+    if (frame >= a.F)
+        return;
+    float* alpha = smem + wv * a.wave_lds_floats; // alpha[s] at alpha + (1 << s)
+    uint32_t* bits = reinterpret_cast<uint32_t*>(alpha + a.N);
+    const float* y = a.llr + frame * a.N;
+    const uint32_t top = a.log2N;
+
+    for (uint32_t k = 0; k < a.nops; ++k) {
+        const uint32_t w = a.ops[k];
+        const uint32_t code = op_code(w), s = op_stage(w), o = op_off(w);
+        if (code >= OP_L_R0) {
+            if (s == top)
+                sc_leaf(code, y, 1u << s, o, bits, lane);
+            else
+                sc_leaf(code, alpha + (1u << s), 1u << s, o, bits, lane);
+        } else if (code == OP_COMB || code == OP_COPY0) {
+            sc_bits_op(code, s, o, bits, lane);
+        } else {
+            if (s == top)
+                sc_inner(code, y, s, o, alpha, bits, lane);
+            else
+                sc_inner(code, alpha + (1u << s), s, o, alpha, bits, lane);
+        }
+        wsync();
+    }
+    if (!a.systematic)
+        polar_transform_bits(bits, a.N, lane);
+    const uint32_t syn = emit_info(bits, a, frame, lane, true);
+    if (lane == 0 && a.ok)
+        a.ok[frame] = syn == 0 ? 1 : 0;
+}
+
+int launch_sc(const KernelArgs& a, hipStream_t stream)
+{
+    constexpr int WAVES = 4;
+    const uint64_t blocks = (a.F + WAVES - 1) / WAVES;
+    if (blocks == 0)
+        return 0;
+    const size_t lds = (size_t)WAVES * a.wave_lds_floats * sizeof(float);
+    hipLaunchKernelGGL(sc_kernel<WAVES>, dim3((uint32_t)blocks), dim3(64 * WAVES), lds, stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+} // namespace pcg

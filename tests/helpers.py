@@ -1,0 +1,47 @@
+"""Shared test data: frozen sets, LLR generators, node-type coverage sets."""
+import numpy as np
+
+
+def llr_kinds(rng, F, N, kind):
+    """LLR families that stress the reference's quirks (ties, +-0, saturation)."""
+    if kind == "normal":
+        return rng.normal(1.0, 1.5, (F, N)).astype(np.float32)
+    if kind == "ints":  # many exact ties and zeros
+        return rng.integers(-3, 4, (F, N)).astype(np.float32)
+    if kind == "zeros":  # +0 / -0 heavy
+        x = rng.normal(0.0, 2.0, (F, N)).astype(np.float32)
+        x[rng.random((F, N)) < 0.2] = -0.0
+        x[rng.random((F, N)) < 0.2] = 0.0
+        return x
+    if kind == "sparse":  # {-1, 0, +1}
+        return (np.sign(rng.normal(0, 1, (F, N))) * rng.integers(0, 2, (F, N))).astype(np.float32)
+    if kind == "wide":  # large dynamic range
+        return (rng.normal(0, 1, (F, N)) * 10.0 ** rng.uniform(-3, 4, (F, N))).astype(np.float32)
+    raise ValueError(kind)
+
+
+LLR_KINDS = ("normal", "ints", "zeros", "sparse", "wide")
+
+
+def node_cover_sets():
+    """(N, frozen) pairs whose Fast-SSC trees contain every leaf kind at several sizes."""
+    out = []
+    # 8-bit specials
+    out.append((8, [0, 1]))                 # DoubleSpcShort8
+    out.append((8, [0, 1, 2]))              # RepRateOne8
+    out.append((8, [0, 1, 2, 3, 4]))        # ZeroSpc8
+    out.append((8, [0, 1, 2, 4]))           # TypeFive n=8
+    out.append((8, [0, 1, 2, 3, 4, 5]))     # DoubleRep n=8
+    for n in (16, 32, 64, 128):
+        out.append((n, [0, 1]))                                  # DoubleSpc
+        out.append((n, list(range(n - 3))))                      # TripleRep
+        out.append((n, sorted(set(range(n - 6)) | {n - 6, n - 4})))  # TypeFive
+        out.append((n, list(range(n - 2))))                      # DoubleRep
+        out.append((n, list(range(n // 2)) + [n // 2]))          # ZeroSpc (Q1)
+        out.append((n, list(range(n // 2 - 1))))                 # ROne at the root
+        out.append((n, list(range(n // 2)) + [n // 2, n // 2 + 1]))  # ZeroR at the root
+    # ShortRateR with n<8 leaves under it
+    out.append((8, [0, 4]))
+    out.append((8, [1, 2, 4]))
+    out.append((16, [0, 2, 8]))
+    return out
