@@ -1,12 +1,796 @@
-// scl_kernel.hip -- batched SCL decoding (placeholder until the list kernel lands).
+// scl_kernel.hip -- batched CRC-aided SCL polar decoding on CDNA4 (gfx950).
+//
+// One codeword per wavefront (one 64-thread workgroup); the wave walks the plan's
+// flattened SCL schedule (SclAvx::createDecoder order, scl_avx_float.cpp:624-651)
+// for all P <= L paths at once.  The reference's PathList/DataPool lazy copies
+// (scl_avx_float.cpp:21-171, datapool.txx) become:
+//   * LLR stage buffers alpha[s][slot] with a per-path slot table ptr[p][s]:
+//     an F/G at stage s rewrites every path's alpha[s] (all old alpha[s] are
+//     dead then), so it writes slot p and resets ptr[p][s] = p; a branching leaf
+//     copies ptr rows (the lazy duplicate) instead of data.  Stages below
+//     `lds_stage_limit` live in LDS, the big top stages in a per-wave global
+//     scratch slab (L2/MALL resident).
+//   * the codeword estimate of each path as packed sign bits with in-place
+//     Combine (observably identical to Bit/LeftBit stage stacks), double
+//     buffered across a branching leaf.
+// Candidate generation, findWeakLlrs and simplePartialSortDescending
+// (arrayfuncs.h:161-231) are simulated exactly -- including their swap-induced
+// tie orders -- with wave argmin/argmax reductions.
 #include "kernels.hpp"
+#include "plan.hpp"
+#include "wave.hpp"
 
 namespace pcg {
-int scl_layout(uint32_t, uint32_t, uint32_t* w, uint32_t* l, uint64_t* s)
+
+namespace {
+
+constexpr uint32_t MAXL = 32;
+constexpr uint32_t MAXC = 8 * MAXL; // candidates per leaf
+
+struct Layout {
+    // float/word offsets inside one wave's LDS slice
+    uint32_t alpha;  // L*(2^S_l - 1) floats
+    uint32_t cw0;    // 2 * L * W words
+    uint32_t ptr;    // 2 * L * 16 bytes (as words)
+    uint32_t met;    // 2 * L floats
+    uint32_t cval;   // MAXC floats
+    uint32_t cid;    // MAXC words
+    uint32_t wk;     // L * 4 floats (weak values)
+    uint32_t wi;     // L * 4 words (weak indices)
+    uint32_t wpar;   // L words
+    uint32_t total;
+};
+
+__host__ __device__ inline Layout make_layout(uint32_t N, uint32_t L, uint32_t Sl)
 {
-    *w = 0; *l = 0; *s = 0;
-    return -4;
+    Layout y;
+    const uint32_t W = N >= 32 ? N / 32 : 1;
+    uint32_t o = 0;
+    y.alpha = o;
+    o += L * ((1u << Sl) - 1u);
+    o = (o + 3) & ~3u;
+    y.cw0 = o;
+    o += 2 * L * W;
+    y.ptr = o;
+    o += 2 * L * 4;
+    y.met = o;
+    o += 2 * L;
+    y.cval = o;
+    o += MAXC;
+    y.cid = o;
+    o += MAXC;
+    y.wk = o;
+    o += 4 * L;
+    y.wi = o;
+    o += 4 * L;
+    y.wpar = o;
+    o += L;
+    y.total = (o + 3) & ~3u;
+    return y;
 }
-uint64_t scl_scratch_frames(uint64_t F) { return F; }
-int launch_scl(const KernelArgs&, hipStream_t) { return -4; }
+
+// alpha slot base (in floats) of stage s inside its storage
+__host__ __device__ inline uint32_t lds_stage_base(uint32_t L, uint32_t s) { return L * ((1u << s) - 1u); }
+__host__ __device__ inline uint64_t gl_stage_base(uint32_t L, uint32_t s, uint32_t Sl)
+{
+    return (uint64_t)L * ((1ull << s) - (1ull << Sl));
+}
+
+struct Ctx {
+    float* lds;             // this wave's LDS slice
+    float* gs;              // this wave's global scratch slab
+    const float* y;         // channel LLRs of the frame
+    uint32_t N, L, top, Sl, W;
+    Layout ly;
+    uint32_t lane;
+};
+
+PCG_DEV uint8_t* ptr_tab(const Ctx& c, uint32_t cur) { return reinterpret_cast<uint8_t*>(c.lds + c.ly.ptr) + cur * c.L * 16; }
+PCG_DEV uint32_t* cw_tab(const Ctx& c, uint32_t cur) { return reinterpret_cast<uint32_t*>(c.lds + c.ly.cw0) + cur * c.L * c.W; }
+PCG_DEV float* met_tab(const Ctx& c, uint32_t cur) { return c.lds + c.ly.met + cur * c.L; }
+
+// ---- stage storage access, address space explicit ---------------------------------
+struct LdsStage {
+    float* b;
+    uint32_t n;
+    PCG_DEV float* slot(uint32_t q) const { return b + q * n; }
+};
+struct GlStage {
+    float* b;
+    uint32_t n;
+    PCG_DEV float* slot(uint32_t q) const { return b + (uint64_t)q * n; }
+};
+struct ChanStage { // the root: channel LLRs, one "slot"
+    const float* y;
+    PCG_DEV const float* slot(uint32_t) const { return y; }
+};
+
+PCG_DEV LdsStage lds_stage(const Ctx& c, uint32_t s) { return LdsStage{ c.lds + c.ly.alpha + lds_stage_base(c.L, s), 1u << s }; }
+PCG_DEV GlStage gl_stage(const Ctx& c, uint32_t s) { return GlStage{ c.gs + gl_stage_base(c.L, s, c.Sl), 1u << s }; }
+
+// ---- internal ops ------------------------------------------------------------------
+// F / G at stage s (node size 2^s): alpha[s-1][p] from alpha[s][ptr[p][s]]
+template <int OPC, typename Src, typename Dst>
+PCG_DEV void fg_op(const Ctx& c, Src src, Dst dst, uint32_t s, uint32_t o, uint32_t P, uint32_t cur)
+{
+    const uint32_t h = 1u << (s - 1), lh = s - 1;
+    const uint8_t* ptr = ptr_tab(c, cur);
+    const uint32_t* cw = cw_tab(c, cur);
+    const uint32_t tot = P << lh;
+    for (uint32_t e = c.lane; e < tot; e += 64) {
+        const uint32_t p = e >> lh, i = e & (h - 1);
+        const auto* in = src.slot(s == c.top ? 0u : ptr[p * 16 + s]);
+        float r;
+        if (OPC == OP_F)
+            r = polar_f(in[i], in[i + h]);
+        else
+            r = polar_g(in[i], in[i + h], get_bit(cw + p * c.W, o + i) << 31);
+        dst.slot(p)[i] = r;
+    }
+}
+
+template <int OPC>
+PCG_DEV void fg_dispatch(const Ctx& c, uint32_t s, uint32_t o, uint32_t P, uint32_t cur)
+{
+    const uint32_t d = s - 1;
+    if (s == c.top) {
+        if (d >= c.Sl)
+            fg_op<OPC>(c, ChanStage{ c.y }, gl_stage(c, d), s, o, P, cur);
+        else
+            fg_op<OPC>(c, ChanStage{ c.y }, lds_stage(c, d), s, o, P, cur);
+    } else if (s >= c.Sl) {
+        if (d >= c.Sl)
+            fg_op<OPC>(c, gl_stage(c, s), gl_stage(c, d), s, o, P, cur);
+        else
+            fg_op<OPC>(c, gl_stage(c, s), lds_stage(c, d), s, o, P, cur);
+    } else {
+        fg_op<OPC>(c, lds_stage(c, s), lds_stage(c, d), s, o, P, cur);
+    }
+    wsync();
+    // every path now owns slot p of stage d
+    uint8_t* ptr = ptr_tab(c, cur);
+    for (uint32_t p = c.lane; p < P; p += 64)
+        ptr[p * 16 + d] = (uint8_t)p;
+}
+
+// COMB at stage s: cw[p][o+i] ^= cw[p][o+h+i], i < h
+PCG_DEV void comb_op(const Ctx& c, uint32_t s, uint32_t o, uint32_t P, uint32_t cur)
+{
+    const uint32_t h = 1u << (s - 1);
+    uint32_t* cw = cw_tab(c, cur);
+    if (h >= 32) {
+        const uint32_t nw = h >> 5, lw = __builtin_ctz(nw);
+        const uint32_t wl = o >> 5, wr = (o + h) >> 5;
+        for (uint32_t e = c.lane; e < (P << lw); e += 64) {
+            const uint32_t p = e >> lw, i = e & (nw - 1);
+            cw[p * c.W + wl + i] ^= cw[p * c.W + wr + i];
+        }
+    } else {
+        const uint32_t sh = o & 31, msk = ((1u << h) - 1u) << sh;
+        for (uint32_t p = c.lane; p < P; p += 64) {
+            uint32_t* w = cw + p * c.W + (o >> 5);
+            *w ^= (*w >> h) & msk;
+        }
+    }
+}
+
+// group helpers: groups of g lanes (power of two <= 64), aligned
+PCG_DEV float group_reduce_add8_ordered(float s, uint32_t lane)
+{
+    // lanes base..base+7 hold s_0..s_7 of one group of 8; every lane of the group gets
+    // ((((((s0+s1)+s2)+s3)+s4)+s5)+s6)+s7
+    const uint32_t base = lane & ~7u;
+    float r = shfl(s, (int)base);
+    for (uint32_t j = 1; j < 8; ++j)
+        r = r + shfl(s, (int)(base + j));
+    return r;
+}
+
+PCG_DEV void group_argmin(float& v, uint32_t& i, uint32_t g)
+{
+    for (uint32_t d = g >> 1; d >= 1; d >>= 1) {
+        const float ov = __shfl_xor(v, (int)d, 64);
+        const uint32_t oi = __shfl_xor(i, (int)d, 64);
+        if (ov < v || (ov == v && oi < i)) {
+            v = ov;
+            i = oi;
+        }
+    }
+}
+
+PCG_DEV uint32_t group_xor(uint32_t v, uint32_t g)
+{
+    for (uint32_t d = g >> 1; d >= 1; d >>= 1)
+        v ^= __shfl_xor(v, (int)d, 64);
+    return v;
+}
+
+// ---- leaves --------------------------------------------------------------------------
+// Rate-0 (scl_avx_float.cpp:316-337): metric += reduce_add(sum_lanes min(llr, +0)); no re-sort.
+template <typename Src>
+PCG_DEV void leaf_r0(const Ctx& c, Src src, uint32_t s, uint32_t o, uint32_t P, uint32_t cur)
+{
+    const uint32_t n = 1u << s;
+    const uint8_t* ptr = ptr_tab(c, cur);
+    float* met = met_tab(c, cur);
+    for (uint32_t p0 = 0; p0 < P; p0 += 8) {
+        const uint32_t p = p0 + (c.lane >> 3), j = c.lane & 7;
+        float acc = 0.0f;
+        if (p < P) {
+            const float* in = src.slot(s == c.top ? 0u : ptr[p * 16 + s]);
+            if (n < 8) {
+                acc = acc + minps(j < n ? in[j] : 0.0f, 0.0f);
+            } else {
+                for (uint32_t i = j; i < n; i += 8)
+                    acc = acc + minps(in[i], 0.0f);
+            }
+        }
+        const float pen = group_reduce_add8_ordered(acc, c.lane);
+        if (p < P && j == 0)
+            met[p] = met[p] + pen;
+    }
+    // bits = +INF -> 0
+    uint32_t* cw = cw_tab(c, cur);
+    if (n >= 32) {
+        const uint32_t nw = n >> 5, lw = __builtin_ctz(nw);
+        for (uint32_t e = c.lane; e < (P << lw); e += 64)
+            cw[(e >> lw) * c.W + (o >> 5) + (e & (nw - 1))] = 0u;
+    } else {
+        const uint32_t msk = ((1u << n) - 1u) << (o & 31);
+        for (uint32_t p = c.lane; p < P; p += 64)
+            cw[p * c.W + (o >> 5)] &= ~msk;
+    }
+}
+
+// Repetition, n < 8 (scl_avx_float.cpp:428-481): 2 candidates per path
+template <typename Src>
+PCG_DEV void cand_rep(const Ctx& c, Src src, uint32_t s, uint32_t P, uint32_t cur)
+{
+    const uint32_t n = 1u << s;
+    const uint8_t* ptr = ptr_tab(c, cur);
+    const float* met = met_tab(c, cur);
+    float* cval = c.lds + c.ly.cval;
+    for (uint32_t p0 = 0; p0 < P; p0 += 8) {
+        const uint32_t p = p0 + (c.lane >> 3), j = c.lane & 7;
+        float l = 0.0f;
+        if (p < P) {
+            const float* in = src.slot(s == c.top ? 0u : ptr[p * 16 + s]);
+            l = j < n ? in[j] : 0.0f;
+        }
+        const float z = 0.0f + minps(l, 0.0f);
+        const float on = 0.0f + maxps(l, 0.0f);
+        const float Z = group_reduce_add8_ordered(z, c.lane);
+        const float O = group_reduce_add8_ordered(on, c.lane);
+        if (p < P && j == 0) {
+            const float m = met[p];
+            cval[2 * p] = m + Z;
+            cval[2 * p + 1] = m - O;
+        }
+    }
+}
+
+// findWeakLlrs(idx, |llr|, n, k) (arrayfuncs.h:209-231) for every path, exact swap
+// semantics, plus the SPC parity (XOR of all n signs).  Results: wk[p][0..k),
+// wi[p][0..k), wpar[p].  Lanes form groups of g = min(n, 64), one path per group.
+template <typename Src>
+PCG_DEV void weak_search(const Ctx& c, Src src, uint32_t s, uint32_t P, uint32_t cur, uint32_t k)
+{
+    const uint32_t n = 1u << s;
+    const uint32_t g = n < 64 ? n : 64;
+    const uint32_t lg = __builtin_ctz(g);
+    const uint32_t gpp = 64 >> lg; // groups per pass
+    const uint32_t gl = c.lane & (g - 1);
+    const uint8_t* ptr = ptr_tab(c, cur);
+    float* wk = c.lds + c.ly.wk;
+    uint32_t* wi = reinterpret_cast<uint32_t*>(c.lds + c.ly.wi);
+    uint32_t* wpar = reinterpret_cast<uint32_t*>(c.lds + c.ly.wpar);
+    const uint32_t lim = (n - 1) < k ? (n - 1) : k;
+    for (uint32_t p0 = 0; p0 < P; p0 += gpp) {
+        const uint32_t p = p0 + (c.lane >> lg);
+        const bool act = p < P;
+        const float* in = src.slot(s == c.top ? 0u : ptr[(act ? p : 0) * 16 + s]);
+        // parity
+        uint32_t par = 0;
+        if (act)
+            for (uint32_t i = gl; i < n; i += g)
+                par ^= fbits(in[i]);
+        par = group_xor(par, g);
+        // overlay of displaced positions (<= 4), identical in every lane of the group
+        uint32_t ovp[4], ovi[4];
+        float ovv[4];
+        uint32_t nov = 0;
+        float T[4];
+        uint32_t I[4];
+        for (uint32_t t = 0; t < lim; ++t) {
+            float bv = __builtin_inff();
+            uint32_t bi = 0xffffffffu;
+            bool first = true;
+            if (act) {
+                for (uint32_t i = gl; i < n; i += g) {
+                    if (i < t)
+                        continue;
+                    bool inov = false;
+                    for (uint32_t q = 0; q < nov; ++q)
+                        inov |= (ovp[q] == i);
+                    if (inov)
+                        continue;
+                    const float v = fabs_(in[i]);
+                    if (first || v < bv) {
+                        bv = v;
+                        bi = i;
+                        first = false;
+                    }
+                }
+            }
+            // overlay candidates (same in every lane of the group; offer them from lane 0 of it)
+            if (gl == 0) {
+                for (uint32_t q = 0; q < nov; ++q) {
+                    if (ovp[q] >= t && (ovv[q] < bv || (ovv[q] == bv && ovp[q] < bi) || bi == 0xffffffffu)) {
+                        bv = ovv[q];
+                        bi = ovp[q];
+                    }
+                }
+            }
+            // NaN-free: an unset lane has (INF, ~0) and loses every tie on the index
+            group_argmin(bv, bi, g);
+            // value / original index at the selected position
+            uint32_t bo = bi;
+            for (uint32_t q = 0; q < nov; ++q)
+                if (ovp[q] == bi)
+                    bo = ovi[q];
+            T[t] = bv;
+            I[t] = bo;
+            // element currently at position t moves to position bi
+            if (bi != t) {
+                float vt = 0.0f;
+                uint32_t it = t;
+                bool tov = false;
+                for (uint32_t q = 0; q < nov; ++q)
+                    if (ovp[q] == t) {
+                        vt = ovv[q];
+                        it = ovi[q];
+                        tov = true;
+                    }
+                if (!tov)
+                    vt = act ? fabs_(in[t]) : 0.0f;
+                bool placed = false;
+                for (uint32_t q = 0; q < nov; ++q)
+                    if (ovp[q] == bi) {
+                        ovv[q] = vt;
+                        ovi[q] = it;
+                        placed = true;
+                    }
+                if (!placed) {
+                    ovp[nov] = bi;
+                    ovv[nov] = vt;
+                    ovi[nov] = it;
+                    ++nov;
+                }
+            }
+        }
+        // passes beyond lim (n-1 < k): the element left at position t
+        for (uint32_t t = lim; t < k; ++t) {
+            float vt = 0.0f;
+            uint32_t it = t;
+            bool tov = false;
+            for (uint32_t q = 0; q < nov; ++q)
+                if (ovp[q] == t) {
+                    vt = ovv[q];
+                    it = ovi[q];
+                    tov = true;
+                }
+            if (!tov)
+                vt = (act && t < n) ? fabs_(in[t]) : __builtin_inff();
+            T[t] = vt;
+            I[t] = it;
+        }
+        if (act && gl == 0) {
+            for (uint32_t t = 0; t < k; ++t) {
+                wk[p * 4 + t] = T[t];
+                wi[p * 4 + t] = I[t];
+            }
+            wpar[p] = par & 0x80000000u;
+        }
+    }
+}
+
+// candidate metrics from the weak values (scl_avx_float.cpp:365-379 and :530-585)
+PCG_DEV void cand_r1_spc(const Ctx& c, uint32_t code, uint32_t P, uint32_t cur)
+{
+    const float* met = met_tab(c, cur);
+    const float* wk = c.lds + c.ly.wk;
+    const uint32_t* wpar = reinterpret_cast<const uint32_t*>(c.lds + c.ly.wpar);
+    float* cval = c.lds + c.ly.cval;
+    const uint32_t k = code == OP_S_R1 ? 4 : 8;
+    for (uint32_t e = c.lane; e < P * k; e += 64) {
+        const uint32_t p = e / k, j = e % k;
+        const float* T = wk + p * 4;
+        float m = met[p];
+        float v;
+        if (code == OP_S_R1) {
+            if (j == 0)
+                v = m;
+            else if (j == 1)
+                v = m - T[0];
+            else if (j == 2)
+                v = m - T[1];
+            else
+                v = m - T[0] - T[1];
+        } else {
+            float pinv = 1.0f;
+            if (wpar[p]) { // odd parity: the reference charges T0 up front
+                pinv = 0.0f;
+                m -= T[0];
+            }
+            switch (j) {
+            case 0: v = m; break;
+            case 1: v = m - pinv * T[0] - T[1]; break;
+            case 2: v = m - pinv * T[0] - T[2]; break;
+            case 3: v = m - pinv * T[0] - T[3]; break;
+            case 4: v = m - T[1] - T[2]; break;
+            case 5: v = m - T[1] - T[3]; break;
+            case 6: v = m - T[2] - T[3]; break;
+            default: v = m - pinv * T[0] - T[1] - T[2] - T[3]; break;
+            }
+        }
+        cval[e] = v;
+    }
+}
+
+// flip mask over the 4 weak indices for candidate j (R1: 4 kinds, SPC: 8 kinds by parity)
+PCG_DEV uint32_t flip_sel(uint32_t code, uint32_t j, uint32_t oddpar)
+{
+    if (code == OP_S_R1) {
+        const uint32_t t[4] = { 0x0, 0x1, 0x2, 0x3 };
+        return t[j];
+    }
+    // bit q set -> flip weak index q
+    const uint32_t ev[8] = { 0x0, 0x3, 0x5, 0x9, 0x6, 0xA, 0xC, 0xF };
+    const uint32_t od[8] = { 0x1, 0x2, 0x4, 0x8, 0x7, 0xB, 0xD, 0xE };
+    return oddpar ? od[j] : ev[j];
+}
+
+// simplePartialSortDescending(idx, cval, np, C) (arrayfuncs.h:161-183): exact swap
+// selection on positions held 4-per-lane (pos = lane + 64 r).  Leaves cid[0..np).
+PCG_DEV void partial_sort(const Ctx& c, uint32_t C, uint32_t np)
+{
+    float* cval = c.lds + c.ly.cval;
+    uint32_t* cid = reinterpret_cast<uint32_t*>(c.lds + c.ly.cid);
+    float v[4];
+    uint32_t id[4];
+    for (uint32_t r = 0; r < 4; ++r) {
+        const uint32_t pos = c.lane + 64 * r;
+        v[r] = pos < C ? cval[pos] : -__builtin_inff();
+        id[r] = pos;
+    }
+    const uint32_t lim = (C - 1) < np ? (C - 1) : np;
+    const uint32_t R = (C + 63) / 64;
+    for (uint32_t t = 0; t < lim; ++t) {
+        float bv = -__builtin_inff();
+        uint32_t bp = 0xffffffffu;
+        for (uint32_t r = 0; r < R; ++r) {
+            const uint32_t pos = c.lane + 64 * r;
+            if (pos >= t && pos < C && (bp == 0xffffffffu || v[r] > bv)) {
+                bv = v[r];
+                bp = pos;
+            }
+        }
+        // max value, ties -> lowest position (first strictly-greater wins)
+        for (int d = 32; d >= 1; d >>= 1) {
+            const float ov = __shfl_xor(bv, d, 64);
+            const uint32_t op = __shfl_xor(bp, d, 64);
+            if (op != 0xffffffffu && (bp == 0xffffffffu || ov > bv || (ov == bv && op < bp))) {
+                bv = ov;
+                bp = op;
+            }
+        }
+        const uint32_t b = __builtin_amdgcn_readfirstlane(bp);
+        if (b == t)
+            continue;
+        // swap positions t and b
+        const uint32_t rt = t >> 6, lt = t & 63, rb = b >> 6, lb = b & 63;
+        float vt = 0, vb = 0;
+        uint32_t it = 0, ib = 0;
+        for (uint32_t r = 0; r < 4; ++r) {
+            const float x = __shfl(v[r], (int)lt, 64);
+            const uint32_t xi = __shfl(id[r], (int)lt, 64);
+            const float y2 = __shfl(v[r], (int)lb, 64);
+            const uint32_t yi = __shfl(id[r], (int)lb, 64);
+            if (r == rt) {
+                vt = x;
+                it = xi;
+            }
+            if (r == rb) {
+                vb = y2;
+                ib = yi;
+            }
+        }
+        for (uint32_t r = 0; r < 4; ++r) {
+            if (r == rt && c.lane == lt) {
+                v[r] = vb;
+                id[r] = ib;
+            }
+            if (r == rb && c.lane == lb) {
+                v[r] = vt;
+                id[r] = it;
+            }
+        }
+    }
+    for (uint32_t r = 0; r < 4; ++r) {
+        const uint32_t pos = c.lane + 64 * r;
+        if (pos < np) {
+            cval[pos] = v[r];
+            cid[pos] = id[r];
+        }
+    }
+}
+
+// Build the next path list after a branching leaf: duplicate (ptr rows + codeword
+// words up to the leaf's end), set metrics, write the leaf's bits.
+template <typename Src>
+PCG_DEV void branch_commit(const Ctx& c, Src src, uint32_t code, uint32_t s, uint32_t o, uint32_t P,
+                           uint32_t np, uint32_t k, uint32_t cur)
+{
+    const uint32_t n = 1u << s, nxt = cur ^ 1u;
+    const uint8_t* ptr = ptr_tab(c, cur);
+    uint8_t* ptr2 = ptr_tab(c, nxt);
+    const uint32_t* cw = cw_tab(c, cur);
+    uint32_t* cw2 = cw_tab(c, nxt);
+    float* met2 = met_tab(c, nxt);
+    const float* cval = c.lds + c.ly.cval;
+    const uint32_t* cid = reinterpret_cast<const uint32_t*>(c.lds + c.ly.cid);
+    const uint32_t* wi = reinterpret_cast<const uint32_t*>(c.lds + c.ly.wi);
+    const uint32_t* wpar = reinterpret_cast<const uint32_t*>(c.lds + c.ly.wpar);
+    // codeword words [0, ceil((o+n)/32)) and ptr rows
+    const uint32_t nw = (o + n + 31) >> 5;
+    for (uint32_t e = c.lane; e < np * nw; e += 64) {
+        const uint32_t q = e / nw, w = e % nw;
+        const uint32_t srcp = cid[q] / k;
+        cw2[q * c.W + w] = cw[srcp * c.W + w];
+    }
+    for (uint32_t e = c.lane; e < np * 4; e += 64) {
+        const uint32_t q = e >> 2, w = e & 3;
+        reinterpret_cast<uint32_t*>(ptr2)[q * 4 + w] = reinterpret_cast<const uint32_t*>(ptr)[(cid[q] / k) * 4 + w];
+    }
+    for (uint32_t q = c.lane; q < np; q += 64)
+        met2[q] = cval[q];
+    wsync();
+    // leaf bits into [o, o+n) of each survivor
+    const uint32_t g = n < 64 ? n : 64;
+    const uint32_t lg = __builtin_ctz(g);
+    const uint32_t gpp = 64 >> lg;
+    for (uint32_t q0 = 0; q0 < np; q0 += gpp) {
+        const uint32_t q = q0 + (c.lane >> lg), gl = c.lane & (g - 1);
+        const bool act = q < np;
+        uint32_t srcp = 0, j = 0, fm = 0;
+        uint32_t wq[4] = { 0, 0, 0, 0 };
+        if (act) {
+            srcp = cid[q] / k;
+            j = cid[q] % k;
+            if (code != OP_S_REP) {
+                fm = flip_sel(code, j, wpar[srcp]);
+                for (uint32_t t = 0; t < 4; ++t)
+                    wq[t] = wi[srcp * 4 + t];
+            }
+        }
+        const float* in = src.slot(s == c.top ? 0u : ptr[(act ? srcp : 0) * 16 + s]);
+        for (uint32_t b = 0; b < n; b += g) {
+            const uint32_t i = b + gl;
+            uint32_t bit = 0;
+            if (act) {
+                if (code == OP_S_REP) {
+                    bit = j; // +|S| -> 0, -|S| -> 1 (also for S == 0: -0.0)
+                } else {
+                    bit = sgn(in[i]) >> 31;
+                    for (uint32_t t = 0; t < 4; ++t)
+                        if (((fm >> t) & 1u) && wq[t] == i)
+                            bit ^= 1u;
+                }
+            }
+            const uint64_t m = ballot(bit != 0);
+            if (g >= 32) {
+                // g = 32 or 64: whole words; lane 0 of each 32-lane half writes
+                const uint32_t half = c.lane >> 5;
+                if ((c.lane & 31) == 0 && act && (g == 64 || true)) {
+                    const uint32_t wv = (uint32_t)(m >> (32 * half));
+                    const uint32_t pos = o + b + (g == 64 ? 32 * half : 0);
+                    cw2[q * c.W + (pos >> 5)] = wv;
+                }
+            } else if (gl == 0 && act) {
+                const uint32_t grp = c.lane >> lg;
+                const uint32_t field = (uint32_t)(m >> (grp * g)) & ((1u << g) - 1u);
+                const uint32_t sh = (o + b) & 31, msk = ((1u << g) - 1u) << sh;
+                uint32_t* w = cw2 + q * c.W + ((o + b) >> 5);
+                *w = (*w & ~msk) | (field << sh);
+            }
+        }
+    }
+}
+
+PCG_DEV void write_bits_from_info(const Ctx& c, const KernelArgs& a, const uint32_t* bits, uint64_t frame, bool write,
+                                  uint32_t* syn)
+{
+    uint32_t sv = 0;
+    for (uint32_t b = c.lane; b < a.kb; b += 64) {
+        uint32_t byte = 0;
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t idx = 8 * b + j;
+            if (idx < a.K) {
+                const uint32_t bit = get_bit(bits, a.info_pos[idx]);
+                byte |= bit << (7 - j);
+                if (bit)
+                    sv ^= a.crc_m[idx];
+            }
+        }
+        if (write)
+            a.info[frame * a.kb + b] = (uint8_t)byte;
+    }
+    *syn = wave_xor(sv) ^ a.crc_c0;
+}
+
+template <typename Fn>
+PCG_DEV void with_src(const Ctx& c, uint32_t s, Fn&& fn)
+{
+    if (s == c.top)
+        fn(ChanStage{ c.y });
+    else if (s >= c.Sl)
+        fn(gl_stage(c, s));
+    else
+        fn(lds_stage(c, s));
+}
+
+} // namespace
+
+__global__ void __launch_bounds__(64) scl_kernel(KernelArgs a)
+{
+    extern __shared__ float smem[];
+    Ctx c;
+    c.lds = smem;
+    c.N = a.N;
+    c.L = a.L;
+    c.top = a.log2N;
+    c.Sl = a.lds_stage_limit;
+    c.W = a.N >= 32 ? a.N / 32 : 1;
+    c.ly = make_layout(a.N, a.L, a.lds_stage_limit);
+    c.lane = threadIdx.x;
+    c.gs = a.scratch ? a.scratch + (uint64_t)blockIdx.x * a.scratch_floats : nullptr;
+
+    for (uint64_t frame = blockIdx.x; frame < a.F; frame += gridDim.x) {
+        c.y = a.llr + frame * a.N;
+        uint32_t cur = 0, P = 1;
+        if (c.lane == 0)
+            met_tab(c, 0)[0] = 0.0f; // a freshly constructed decoder
+        wsync();
+        for (uint32_t kop = 0; kop < a.nops; ++kop) {
+            const uint32_t w = a.ops[kop];
+            const uint32_t code = op_code(w), s = op_stage(w), o = op_off(w);
+            switch (code) {
+            case OP_F:
+                fg_dispatch<OP_F>(c, s, o, P, cur);
+                break;
+            case OP_G:
+                fg_dispatch<OP_G>(c, s, o, P, cur);
+                break;
+            case OP_COMB:
+                comb_op(c, s, o, P, cur);
+                break;
+            case OP_S_R0:
+                with_src(c, s, [&](auto src) { leaf_r0(c, src, s, o, P, cur); });
+                break;
+            default: { // branching leaves
+                const uint32_t k = code == OP_S_R1 ? 4 : code == OP_S_SPC ? 8 : 2;
+                if (code == OP_S_REP) {
+                    with_src(c, s, [&](auto src) { cand_rep(c, src, s, P, cur); });
+                } else {
+                    with_src(c, s, [&](auto src) { weak_search(c, src, s, P, cur, code == OP_S_R1 ? 2 : 4); });
+                    wsync();
+                    cand_r1_spc(c, code, P, cur);
+                }
+                wsync();
+                const uint32_t C = P * k;
+                const uint32_t np = C < c.L ? C : c.L;
+                partial_sort(c, C, np);
+                wsync();
+                with_src(c, s, [&](auto src) { branch_commit(c, src, code, s, o, P, np, k, cur); });
+                cur ^= 1u;
+                P = np;
+                break;
+            }
+            }
+            wsync();
+        }
+        // extractBestPath (scl_avx_float.cpp:711-750): first path in list order whose
+        // detector check passes, else path 0.
+        uint32_t* cwc = cw_tab(c, cur);
+        if (!a.systematic) {
+            // re-encode every path in place (G_N is applied per path)
+            const uint32_t M[5] = { 0x55555555u, 0x33333333u, 0x0F0F0F0Fu, 0x00FF00FFu, 0x0000FFFFu };
+            for (uint32_t e = c.lane; e < P * c.W; e += 64) {
+                uint32_t x = cwc[e];
+                for (uint32_t kk = 0, B = 1; kk < 5 && B < c.N; ++kk, B <<= 1)
+                    x ^= (x >> B) & M[kk];
+                cwc[e] = x;
+            }
+            wsync();
+            for (uint32_t d = 1; d < c.W; d <<= 1) {
+                for (uint32_t e = c.lane; e < P * c.W; e += 64) {
+                    const uint32_t wi2 = e % c.W;
+                    if (!(wi2 & d))
+                        cwc[e] ^= cwc[e + d];
+                }
+                wsync();
+            }
+        }
+        uint32_t chosen = 0, found = 0;
+        for (uint32_t p = 0; p < P; ++p) {
+            uint32_t syn;
+            write_bits_from_info(c, a, cwc + p * c.W, frame, false, &syn);
+            if (syn == 0) {
+                chosen = p;
+                found = 1;
+                break;
+            }
+        }
+        uint32_t dummy;
+        write_bits_from_info(c, a, cwc + chosen * c.W, frame, true, &dummy);
+        if (c.lane == 0 && a.ok)
+            a.ok[frame] = (uint8_t)found;
+        if (a.metrics) {
+            const float* met = met_tab(c, cur);
+            for (uint32_t p = c.lane; p < c.L; p += 64)
+                a.metrics[frame * c.L + p] = p < P ? met[p] : 0.0f;
+        }
+        wsync();
+    }
+}
+
+int scl_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* lds_stage_limit, uint64_t* scratch_floats)
+{
+    if (L < 2 || L > MAXL)
+        return -4;
+    const uint32_t top = (uint32_t)__builtin_ctz(N);
+    // Largest LDS-resident stage set within the budget; the rest goes to global scratch.
+    uint32_t budget = 24 * 1024 / 4; // floats per wave (~6 codewords per CU)
+    if (const char* e = getenv("PCG_SCL_LDS_KB"))
+        budget = (uint32_t)atoi(e) * 1024 / 4;
+    uint32_t Sl = top;
+    while (Sl > 1 && make_layout(N, L, Sl).total > budget)
+        --Sl;
+    if (const char* e = getenv("PCG_SCL_STAGE_LIMIT")) {
+        uint32_t v = (uint32_t)atoi(e);
+        if (v >= 1 && v <= top)
+            Sl = v;
+    }
+    const Layout ly = make_layout(N, L, Sl);
+    if (ly.total * 4 > 160 * 1024)
+        return -4;
+    *wave_lds_floats = ly.total;
+    *lds_stage_limit = Sl;
+    *scratch_floats = (uint64_t)L * ((1ull << top) - (1ull << Sl));
+    return 0;
+}
+
+static uint64_t g_resident_cap = 0;
+
+uint64_t scl_scratch_frames(uint64_t F)
+{
+    if (g_resident_cap == 0) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess)
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        g_resident_cap = (uint64_t)cus * 16; // grid cap (grid-stride over frames)
+    }
+    return F < g_resident_cap ? F : g_resident_cap;
+}
+
+int launch_scl(const KernelArgs& a, hipStream_t stream)
+{
+    const uint64_t grid = scl_scratch_frames(a.F);
+    if (grid == 0)
+        return 0;
+    const size_t lds = (size_t)a.wave_lds_floats * sizeof(float);
+    hipLaunchKernelGGL(scl_kernel, dim3((uint32_t)grid), dim3(64), lds, stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 } // namespace pcg
