@@ -33,6 +33,7 @@ struct pcg_plan {
 namespace {
 
 thread_local std::string g_last_error;
+unsigned long long* g_prof = nullptr; // dev-only op profiler buffer (PCG_OPPROF=1)
 
 int fail(int code, const std::string& msg)
 {
@@ -77,6 +78,22 @@ void free_plan_device(pcg_plan* p)
 extern "C" {
 
 const char* pcg_last_error(void) { return g_last_error.c_str(); }
+
+// Development aid, not part of include/pcg.h: with PCG_OPPROF=1 in the environment
+// the kernels accumulate s_memtime cycles and counts per op code; this copies the
+// 64 x {cycles, count} table out and clears it.
+int pcg_dev_opprof_fetch(unsigned long long* out128)
+{
+    if (!g_prof) {
+        std::memset(out128, 0, 128 * sizeof(unsigned long long));
+        return PCG_OK;
+    }
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(out128, g_prof, 128 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        return fail(PCG_E_HIP, "opprof copy failed");
+    (void)hipMemset(g_prof, 0, 128 * sizeof(unsigned long long));
+    return PCG_OK;
+}
 
 int pcg_device_count(void)
 {
@@ -211,6 +228,11 @@ int pcg_decode_f32(pcg_plan* p,
     a.wave_lds_floats = p->wave_lds_floats;
     a.lds_stage_limit = p->lds_stage_limit;
     a.scratch_floats = p->scratch_floats;
+    if (getenv("PCG_OPPROF")) {
+        if (!g_prof && hipMalloc(&g_prof, 128 * sizeof(unsigned long long)) == hipSuccess)
+            (void)hipMemset(g_prof, 0, 128 * sizeof(unsigned long long));
+        a.prof = g_prof;
+    }
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc;
     if (h.L == 1) {

@@ -22,6 +22,7 @@ struct KernelArgs {
     float* scratch;           // global per-codeword scratch (SCL large stages)
     uint64_t scratch_floats;  // per codeword
     uint32_t lds_stage_limit; // SCL: stages < limit live in LDS
+    unsigned long long* prof; // dev-only: per-op-code [cycles, count] (null = off)
 };
 
 // LDS floats one SC codeword needs: alpha (N floats, index 0 unused) + packed bits.

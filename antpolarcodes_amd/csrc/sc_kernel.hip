@@ -343,13 +343,8 @@ PCG_DEV void sc_bits_op(uint32_t code, uint32_t s, uint32_t o, uint32_t* bits, u
 PCG_DEV void polar_transform_bits(uint32_t* bits, uint32_t N, uint32_t lane)
 {
     const uint32_t W = N >= 32 ? N / 32 : 1;
-    const uint32_t M[5] = { 0x55555555u, 0x33333333u, 0x0F0F0F0Fu, 0x00FF00FFu, 0x0000FFFFu };
-    for (uint32_t i = lane; i < W; i += 64) {
-        uint32_t w = bits[i];
-        for (uint32_t k = 0, B = 1; k < 5 && B < N; ++k, B <<= 1)
-            w ^= (w >> B) & M[k];
-        bits[i] = w;
-    }
+    for (uint32_t i = lane; i < W; i += 64)
+        bits[i] = transform_word(bits[i], N);
     wsync();
     for (uint32_t d = 1; d < W; d <<= 1) {
         for (uint32_t i = lane; i < W; i += 64)
@@ -397,6 +392,7 @@ __global__ void __launch_bounds__(64 * WAVES) sc_kernel(KernelArgs a)
     for (uint32_t k = 0; k < a.nops; ++k) {
         const uint32_t w = a.ops[k];
         const uint32_t code = op_code(w), s = op_stage(w), o = op_off(w);
+        const uint64_t t0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
         if (code >= OP_L_R0) {
             if (s == top)
                 sc_leaf(code, y, 1u << s, o, bits, lane);
@@ -411,6 +407,13 @@ __global__ void __launch_bounds__(64 * WAVES) sc_kernel(KernelArgs a)
                 sc_inner(code, alpha + (1u << s), s, o, alpha, bits, lane);
         }
         wsync();
+        if (a.prof) {
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            if (lane == 0) {
+                atomicAdd(&a.prof[2 * code], (unsigned long long)(t1 - t0));
+                atomicAdd(&a.prof[2 * code + 1], 1ull);
+            }
+        }
     }
     if (!a.systematic)
         polar_transform_bits(bits, a.N, lane);

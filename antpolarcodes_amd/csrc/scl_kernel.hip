@@ -38,16 +38,23 @@ struct Layout {
     uint32_t wk;     // L * 4 floats (weak values)
     uint32_t wi;     // L * 4 words (weak indices)
     uint32_t wpar;   // L words
+    uint32_t xch;    // 64 floats lane exchange
     uint32_t total;
 };
 
+// alpha slot base (in floats) of stage s inside its storage.  LDS slots are
+// max(2^s, 4) floats so every stage and slot is 16-byte aligned (float4 access).
+__host__ __device__ inline uint32_t lds_stage_base(uint32_t L, uint32_t s)
+{
+    return s == 0 ? 0u : s == 1 ? 4u * L : L * ((1u << s) + 4u);
+}
 __host__ __device__ inline Layout make_layout(uint32_t N, uint32_t L, uint32_t Sl)
 {
     Layout y;
     const uint32_t W = N >= 32 ? N / 32 : 1;
     uint32_t o = 0;
     y.alpha = o;
-    o += L * ((1u << Sl) - 1u);
+    o += lds_stage_base(L, Sl);
     o = (o + 3) & ~3u;
     y.cw0 = o;
     o += 2 * L * W;
@@ -65,12 +72,13 @@ __host__ __device__ inline Layout make_layout(uint32_t N, uint32_t L, uint32_t S
     o += 4 * L;
     y.wpar = o;
     o += L;
+    o = (o + 3) & ~3u;
+    y.xch = o;
+    o += 64;
     y.total = (o + 3) & ~3u;
     return y;
 }
 
-// alpha slot base (in floats) of stage s inside its storage
-__host__ __device__ inline uint32_t lds_stage_base(uint32_t L, uint32_t s) { return L * ((1u << s) - 1u); }
 __host__ __device__ inline uint64_t gl_stage_base(uint32_t L, uint32_t s, uint32_t Sl)
 {
     return (uint64_t)L * ((1ull << s) - (1ull << Sl));
@@ -105,11 +113,16 @@ struct ChanStage { // the root: channel LLRs, one "slot"
     PCG_DEV const float* slot(uint32_t) const { return y; }
 };
 
-PCG_DEV LdsStage lds_stage(const Ctx& c, uint32_t s) { return LdsStage{ c.lds + c.ly.alpha + lds_stage_base(c.L, s), 1u << s }; }
+PCG_DEV LdsStage lds_stage(const Ctx& c, uint32_t s)
+{
+    return LdsStage{ c.lds + c.ly.alpha + lds_stage_base(c.L, s), s >= 2 ? (1u << s) : 4u };
+}
 PCG_DEV GlStage gl_stage(const Ctx& c, uint32_t s) { return GlStage{ c.gs + gl_stage_base(c.L, s, c.Sl), 1u << s }; }
 
 // ---- internal ops ------------------------------------------------------------------
-// F / G at stage s (node size 2^s): alpha[s-1][p] from alpha[s][ptr[p][s]]
+// F / G at stage s (node size 2^s): alpha[s-1][p] from alpha[s][ptr[p][s]].
+// Flattened over (path, i); for h >= 4 each lane owns 4 consecutive i (float4), and
+// up to 4 such chunks are loaded before any store so LDS latency overlaps.
 template <int OPC, typename Src, typename Dst>
 PCG_DEV void fg_op(const Ctx& c, Src src, Dst dst, uint32_t s, uint32_t o, uint32_t P, uint32_t cur)
 {
@@ -117,15 +130,54 @@ PCG_DEV void fg_op(const Ctx& c, Src src, Dst dst, uint32_t s, uint32_t o, uint3
     const uint8_t* ptr = ptr_tab(c, cur);
     const uint32_t* cw = cw_tab(c, cur);
     const uint32_t tot = P << lh;
-    for (uint32_t e = c.lane; e < tot; e += 64) {
-        const uint32_t p = e >> lh, i = e & (h - 1);
-        const auto* in = src.slot(s == c.top ? 0u : ptr[p * 16 + s]);
-        float r;
-        if (OPC == OP_F)
-            r = polar_f(in[i], in[i + h]);
-        else
-            r = polar_g(in[i], in[i + h], get_bit(cw + p * c.W, o + i) << 31);
-        dst.slot(p)[i] = r;
+    if (h >= 4) {
+        for (uint32_t e0 = 4 * c.lane; e0 < tot; e0 += 4 * 256) {
+            float4 xa[4], xb[4];
+            uint32_t wb[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t e = e0 + 256 * u;
+                if (e < tot) {
+                    const uint32_t p = e >> lh, i = e & (h - 1);
+                    const auto* in = src.slot(s == c.top ? 0u : ptr[p * 16 + s]);
+                    xa[u] = *reinterpret_cast<const float4*>(in + i);
+                    xb[u] = *reinterpret_cast<const float4*>(in + i + h);
+                    if (OPC == OP_G)
+                        wb[u] = cw[p * c.W + ((o + i) >> 5)] >> ((o + i) & 31);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t e = e0 + 256 * u;
+                if (e < tot) {
+                    const uint32_t p = e >> lh, i = e & (h - 1);
+                    float4 r;
+                    if (OPC == OP_F) {
+                        r.x = polar_f(xa[u].x, xb[u].x);
+                        r.y = polar_f(xa[u].y, xb[u].y);
+                        r.z = polar_f(xa[u].z, xb[u].z);
+                        r.w = polar_f(xa[u].w, xb[u].w);
+                    } else {
+                        r.x = polar_g(xa[u].x, xb[u].x, (wb[u] & 1u) << 31);
+                        r.y = polar_g(xa[u].y, xb[u].y, ((wb[u] >> 1) & 1u) << 31);
+                        r.z = polar_g(xa[u].z, xb[u].z, ((wb[u] >> 2) & 1u) << 31);
+                        r.w = polar_g(xa[u].w, xb[u].w, ((wb[u] >> 3) & 1u) << 31);
+                    }
+                    *reinterpret_cast<float4*>(dst.slot(p) + i) = r;
+                }
+            }
+        }
+    } else {
+        for (uint32_t e = c.lane; e < tot; e += 64) {
+            const uint32_t p = e >> lh, i = e & (h - 1);
+            const auto* in = src.slot(s == c.top ? 0u : ptr[p * 16 + s]);
+            float r;
+            if (OPC == OP_F)
+                r = polar_f(in[i], in[i + h]);
+            else
+                r = polar_g(in[i], in[i + h], get_bit(cw + p * c.W, o + i) << 31);
+            dst.slot(p)[i] = r;
+        }
     }
 }
 
@@ -174,35 +226,29 @@ PCG_DEV void comb_op(const Ctx& c, uint32_t s, uint32_t o, uint32_t P, uint32_t 
     }
 }
 
-// group helpers: groups of g lanes (power of two <= 64), aligned
-PCG_DEV float group_reduce_add8_ordered(float s, uint32_t lane)
+// Ordered 8-lane sum ((((((s0+s1)+s2)+s3)+s4)+s5)+s6)+s7 of aligned 8-lane groups
+// (reduce_add_ps, avxconvenience.h:256-272), through the wave's LDS exchange area.
+// Valid in the first lane of each group.
+PCG_DEV float ordered_sum8(const Ctx& c, float s)
 {
-    // lanes base..base+7 hold s_0..s_7 of one group of 8; every lane of the group gets
-    // ((((((s0+s1)+s2)+s3)+s4)+s5)+s6)+s7
-    const uint32_t base = lane & ~7u;
-    float r = shfl(s, (int)base);
-    for (uint32_t j = 1; j < 8; ++j)
-        r = r + shfl(s, (int)(base + j));
-    return r;
-}
-
-PCG_DEV void group_argmin(float& v, uint32_t& i, uint32_t g)
-{
-    for (uint32_t d = g >> 1; d >= 1; d >>= 1) {
-        const float ov = __shfl_xor(v, (int)d, 64);
-        const uint32_t oi = __shfl_xor(i, (int)d, 64);
-        if (ov < v || (ov == v && oi < i)) {
-            v = ov;
-            i = oi;
-        }
+    float* x = c.lds + c.ly.xch;
+    x[c.lane] = s;
+    wsync();
+    float r = 0.0f;
+    if ((c.lane & 7) == 0) {
+        const float4 a = *reinterpret_cast<const float4*>(x + c.lane);
+        const float4 b = *reinterpret_cast<const float4*>(x + c.lane + 4);
+        r = a.x;
+        r = r + a.y;
+        r = r + a.z;
+        r = r + a.w;
+        r = r + b.x;
+        r = r + b.y;
+        r = r + b.z;
+        r = r + b.w;
     }
-}
-
-PCG_DEV uint32_t group_xor(uint32_t v, uint32_t g)
-{
-    for (uint32_t d = g >> 1; d >= 1; d >>= 1)
-        v ^= __shfl_xor(v, (int)d, 64);
-    return v;
+    wsync();
+    return r;
 }
 
 // ---- leaves --------------------------------------------------------------------------
@@ -225,7 +271,7 @@ PCG_DEV void leaf_r0(const Ctx& c, Src src, uint32_t s, uint32_t o, uint32_t P, 
                     acc = acc + minps(in[i], 0.0f);
             }
         }
-        const float pen = group_reduce_add8_ordered(acc, c.lane);
+        const float pen = ordered_sum8(c, acc);
         if (p < P && j == 0)
             met[p] = met[p] + pen;
     }
@@ -259,8 +305,8 @@ PCG_DEV void cand_rep(const Ctx& c, Src src, uint32_t s, uint32_t P, uint32_t cu
         }
         const float z = 0.0f + minps(l, 0.0f);
         const float on = 0.0f + maxps(l, 0.0f);
-        const float Z = group_reduce_add8_ordered(z, c.lane);
-        const float O = group_reduce_add8_ordered(on, c.lane);
+        const float Z = ordered_sum8(c, z);
+        const float O = ordered_sum8(c, on);
         if (p < P && j == 0) {
             const float m = met[p];
             cval[2 * p] = m + Z;
@@ -271,14 +317,23 @@ PCG_DEV void cand_rep(const Ctx& c, Src src, uint32_t s, uint32_t P, uint32_t cu
 
 // findWeakLlrs(idx, |llr|, n, k) (arrayfuncs.h:209-231) for every path, exact swap
 // semantics, plus the SPC parity (XOR of all n signs).  Results: wk[p][0..k),
-// wi[p][0..k), wpar[p].  Lanes form groups of g = min(n, 64), one path per group.
+// wi[p][0..k), wpar[p].  All paths run together: groups of g lanes per path
+// (g = min(n, max(64/P2, 8))), each lane scanning positions gl, gl+g, ...  The
+// selection-sort swaps are tracked as an overlay of <= k displaced positions.
 template <typename Src>
 PCG_DEV void weak_search(const Ctx& c, Src src, uint32_t s, uint32_t P, uint32_t cur, uint32_t k)
 {
     const uint32_t n = 1u << s;
-    const uint32_t g = n < 64 ? n : 64;
+    uint32_t P2 = 1;
+    while (P2 < P)
+        P2 <<= 1;
+    uint32_t g = 64 / P2;
+    if (g < 8)
+        g = 8;
+    if (g > n)
+        g = n;
     const uint32_t lg = __builtin_ctz(g);
-    const uint32_t gpp = 64 >> lg; // groups per pass
+    const uint32_t gpp = 64 >> lg; // paths per pass
     const uint32_t gl = c.lane & (g - 1);
     const uint8_t* ptr = ptr_tab(c, cur);
     float* wk = c.lds + c.ly.wk;
@@ -289,108 +344,95 @@ PCG_DEV void weak_search(const Ctx& c, Src src, uint32_t s, uint32_t P, uint32_t
         const uint32_t p = p0 + (c.lane >> lg);
         const bool act = p < P;
         const float* in = src.slot(s == c.top ? 0u : ptr[(act ? p : 0) * 16 + s]);
-        // parity
         uint32_t par = 0;
         if (act)
             for (uint32_t i = gl; i < n; i += g)
                 par ^= fbits(in[i]);
-        par = group_xor(par, g);
-        // overlay of displaced positions (<= 4), identical in every lane of the group
-        uint32_t ovp[4], ovi[4];
-        float ovv[4];
-        uint32_t nov = 0;
-        float T[4];
-        uint32_t I[4];
+        par = grp_xor(par, g);
+        uint32_t ovp[4] = { ~0u, ~0u, ~0u, ~0u }, ovi[4] = { 0, 0, 0, 0 };
+        float ovv[4] = { 0, 0, 0, 0 };
+        const bool wr = act && gl == 0;
         for (uint32_t t = 0; t < lim; ++t) {
             float bv = __builtin_inff();
             uint32_t bi = 0xffffffffu;
-            bool first = true;
             if (act) {
                 for (uint32_t i = gl; i < n; i += g) {
-                    if (i < t)
-                        continue;
-                    bool inov = false;
-                    for (uint32_t q = 0; q < nov; ++q)
-                        inov |= (ovp[q] == i);
-                    if (inov)
-                        continue;
+                    const bool inov = (i == ovp[0]) | (i == ovp[1]) | (i == ovp[2]) | (i == ovp[3]);
                     const float v = fabs_(in[i]);
-                    if (first || v < bv) {
+                    if (i >= t && !inov && (bi == 0xffffffffu || v < bv)) {
                         bv = v;
                         bi = i;
-                        first = false;
+                    }
+                }
+                if (gl == 0) {
+#pragma unroll
+                    for (uint32_t q = 0; q < 4; ++q) {
+                        if (ovp[q] != ~0u && ovp[q] >= t &&
+                            (bi == 0xffffffffu || ovv[q] < bv || (ovv[q] == bv && ovp[q] < bi))) {
+                            bv = ovv[q];
+                            bi = ovp[q];
+                        }
                     }
                 }
             }
-            // overlay candidates (same in every lane of the group; offer them from lane 0 of it)
-            if (gl == 0) {
-                for (uint32_t q = 0; q < nov; ++q) {
-                    if (ovp[q] >= t && (ovv[q] < bv || (ovv[q] == bv && ovp[q] < bi) || bi == 0xffffffffu)) {
-                        bv = ovv[q];
-                        bi = ovp[q];
-                    }
-                }
-            }
-            // NaN-free: an unset lane has (INF, ~0) and loses every tie on the index
-            group_argmin(bv, bi, g);
-            // value / original index at the selected position
+            grp_argmin(bv, bi, g);
             uint32_t bo = bi;
-            for (uint32_t q = 0; q < nov; ++q)
+            float vt = 0.0f;
+            uint32_t it = t;
+            bool tov = false;
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) {
                 if (ovp[q] == bi)
                     bo = ovi[q];
-            T[t] = bv;
-            I[t] = bo;
-            // element currently at position t moves to position bi
-            if (bi != t) {
-                float vt = 0.0f;
-                uint32_t it = t;
-                bool tov = false;
-                for (uint32_t q = 0; q < nov; ++q)
-                    if (ovp[q] == t) {
-                        vt = ovv[q];
-                        it = ovi[q];
-                        tov = true;
-                    }
+                if (ovp[q] == t) {
+                    vt = ovv[q];
+                    it = ovi[q];
+                    tov = true;
+                }
+            }
+            if (wr) {
+                wk[p * 4 + t] = bv;
+                wi[p * 4 + t] = bo;
+            }
+            if (bi != t) { // the element at position t moves to position bi
                 if (!tov)
                     vt = act ? fabs_(in[t]) : 0.0f;
                 bool placed = false;
-                for (uint32_t q = 0; q < nov; ++q)
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q)
                     if (ovp[q] == bi) {
                         ovv[q] = vt;
                         ovi[q] = it;
                         placed = true;
                     }
                 if (!placed) {
-                    ovp[nov] = bi;
-                    ovv[nov] = vt;
-                    ovi[nov] = it;
-                    ++nov;
+#pragma unroll
+                    for (uint32_t q = 0; q < 4; ++q)
+                        if (q == t) { // pass t adds at most overlay entry t
+                            ovp[q] = bi;
+                            ovv[q] = vt;
+                            ovi[q] = it;
+                        }
                 }
             }
         }
-        // passes beyond lim (n-1 < k): the element left at position t
+        // positions left after lim passes (n-1 < k)
         for (uint32_t t = lim; t < k; ++t) {
-            float vt = 0.0f;
+            float vt = (act && t < n) ? fabs_(in[t]) : __builtin_inff();
             uint32_t it = t;
-            bool tov = false;
-            for (uint32_t q = 0; q < nov; ++q)
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q)
                 if (ovp[q] == t) {
                     vt = ovv[q];
                     it = ovi[q];
-                    tov = true;
                 }
-            if (!tov)
-                vt = (act && t < n) ? fabs_(in[t]) : __builtin_inff();
-            T[t] = vt;
-            I[t] = it;
-        }
-        if (act && gl == 0) {
-            for (uint32_t t = 0; t < k; ++t) {
-                wk[p * 4 + t] = T[t];
-                wi[p * 4 + t] = I[t];
+            if (wr) {
+                wk[p * 4 + t] = vt;
+                wi[p * 4 + t] = it;
             }
-            wpar[p] = par & 0x80000000u;
         }
+        if (wr)
+            wpar[p] = par & 0x80000000u;
     }
 }
 
@@ -437,92 +479,105 @@ PCG_DEV void cand_r1_spc(const Ctx& c, uint32_t code, uint32_t P, uint32_t cur)
     }
 }
 
-// flip mask over the 4 weak indices for candidate j (R1: 4 kinds, SPC: 8 kinds by parity)
+// flip mask over the 4 weak indices for candidate j, one nibble per candidate:
+// R1 {}, {i0}, {i1}, {i0,i1};  SPC even parity {}, {0,1}, {0,2}, {0,3}, {1,2}, {1,3},
+// {2,3}, {0,1,2,3};  SPC odd parity {0}, {1}, {2}, {3}, {0,1,2}, {0,1,3}, {0,2,3}, {1,2,3}
+// (scl_avx_float.cpp:375-378 and 533-585).
 PCG_DEV uint32_t flip_sel(uint32_t code, uint32_t j, uint32_t oddpar)
 {
-    if (code == OP_S_R1) {
-        const uint32_t t[4] = { 0x0, 0x1, 0x2, 0x3 };
-        return t[j];
-    }
-    // bit q set -> flip weak index q
-    const uint32_t ev[8] = { 0x0, 0x3, 0x5, 0x9, 0x6, 0xA, 0xC, 0xF };
-    const uint32_t od[8] = { 0x1, 0x2, 0x4, 0x8, 0x7, 0xB, 0xD, 0xE };
-    return oddpar ? od[j] : ev[j];
+    const uint32_t tab = code == OP_S_R1 ? 0x3210u : oddpar ? 0xEDB78421u : 0xFCA69530u;
+    return (tab >> (4 * j)) & 0xFu;
 }
 
 // simplePartialSortDescending(idx, cval, np, C) (arrayfuncs.h:161-183): exact swap
-// selection on positions held 4-per-lane (pos = lane + 64 r).  Leaves cid[0..np).
-PCG_DEV void partial_sort(const Ctx& c, uint32_t C, uint32_t np)
+// selection, positions held R-per-lane (pos = lane + 64 r) in named registers (no
+// private arrays), DPP argmax per pass, swaps through readlane.  Leaves cval/cid[0..np).
+template <int R>
+PCG_DEV void partial_sort_r(const Ctx& c, uint32_t C, uint32_t np)
 {
     float* cval = c.lds + c.ly.cval;
     uint32_t* cid = reinterpret_cast<uint32_t*>(c.lds + c.ly.cid);
-    float v[4];
-    uint32_t id[4];
-    for (uint32_t r = 0; r < 4; ++r) {
-        const uint32_t pos = c.lane + 64 * r;
-        v[r] = pos < C ? cval[pos] : -__builtin_inff();
-        id[r] = pos;
+    const uint32_t l = c.lane;
+    float v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+    uint32_t i0 = l, i1 = l + 64, i2 = l + 128, i3 = l + 192;
+    v0 = l < C ? cval[l] : 0.0f;
+    if (R > 1) {
+        v1 = l + 64 < C ? cval[l + 64] : 0.0f;
+        v2 = l + 128 < C ? cval[l + 128] : 0.0f;
+        v3 = l + 192 < C ? cval[l + 192] : 0.0f;
     }
     const uint32_t lim = (C - 1) < np ? (C - 1) : np;
-    const uint32_t R = (C + 63) / 64;
     for (uint32_t t = 0; t < lim; ++t) {
-        float bv = -__builtin_inff();
+        float bv = 0.0f;
         uint32_t bp = 0xffffffffu;
-        for (uint32_t r = 0; r < R; ++r) {
-            const uint32_t pos = c.lane + 64 * r;
-            if (pos >= t && pos < C && (bp == 0xffffffffu || v[r] > bv)) {
-                bv = v[r];
+        auto offer = [&](float v, uint32_t pos) {
+            if (pos >= t && pos < C && (bp == 0xffffffffu || v > bv)) {
+                bv = v;
                 bp = pos;
             }
+        };
+        offer(v0, l);
+        if (R > 1) {
+            offer(v1, l + 64);
+            offer(v2, l + 128);
+            offer(v3, l + 192);
         }
-        // max value, ties -> lowest position (first strictly-greater wins)
-        for (int d = 32; d >= 1; d >>= 1) {
-            const float ov = __shfl_xor(bv, d, 64);
-            const uint32_t op = __shfl_xor(bp, d, 64);
-            if (op != 0xffffffffu && (bp == 0xffffffffu || ov > bv || (ov == bv && op < bp))) {
-                bv = ov;
-                bp = op;
-            }
-        }
+        wave_argmax_dpp(bv, bp);
         const uint32_t b = __builtin_amdgcn_readfirstlane(bp);
         if (b == t)
             continue;
-        // swap positions t and b
         const uint32_t rt = t >> 6, lt = t & 63, rb = b >> 6, lb = b & 63;
-        float vt = 0, vb = 0;
-        uint32_t it = 0, ib = 0;
-        for (uint32_t r = 0; r < 4; ++r) {
-            const float x = __shfl(v[r], (int)lt, 64);
-            const uint32_t xi = __shfl(id[r], (int)lt, 64);
-            const float y2 = __shfl(v[r], (int)lb, 64);
-            const uint32_t yi = __shfl(id[r], (int)lb, 64);
-            if (r == rt) {
-                vt = x;
-                it = xi;
+        auto rdv = [&](uint32_t r, uint32_t ln) -> float {
+            float x = ubits((uint32_t)__builtin_amdgcn_readlane((int)fbits(v0), (int)ln));
+            if (R > 1) {
+                const float x1 = ubits((uint32_t)__builtin_amdgcn_readlane((int)fbits(v1), (int)ln));
+                const float x2 = ubits((uint32_t)__builtin_amdgcn_readlane((int)fbits(v2), (int)ln));
+                const float x3 = ubits((uint32_t)__builtin_amdgcn_readlane((int)fbits(v3), (int)ln));
+                x = r == 1 ? x1 : r == 2 ? x2 : r == 3 ? x3 : x;
             }
-            if (r == rb) {
-                vb = y2;
-                ib = yi;
+            return x;
+        };
+        auto rdi = [&](uint32_t r, uint32_t ln) -> uint32_t {
+            uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)i0, (int)ln);
+            if (R > 1) {
+                const uint32_t x1 = (uint32_t)__builtin_amdgcn_readlane((int)i1, (int)ln);
+                const uint32_t x2 = (uint32_t)__builtin_amdgcn_readlane((int)i2, (int)ln);
+                const uint32_t x3 = (uint32_t)__builtin_amdgcn_readlane((int)i3, (int)ln);
+                x = r == 1 ? x1 : r == 2 ? x2 : r == 3 ? x3 : x;
             }
-        }
-        for (uint32_t r = 0; r < 4; ++r) {
-            if (r == rt && c.lane == lt) {
-                v[r] = vb;
-                id[r] = ib;
-            }
-            if (r == rb && c.lane == lb) {
-                v[r] = vt;
-                id[r] = it;
-            }
+            return x;
+        };
+        const float vt = rdv(rt, lt), vb = rdv(rb, lb);
+        const uint32_t it = rdi(rt, lt), ib = rdi(rb, lb);
+        const bool at_t = l == lt, at_b = l == lb;
+        if (rt == 0 && at_t) { v0 = vb; i0 = ib; }
+        if (rb == 0 && at_b) { v0 = vt; i0 = it; }
+        if (R > 1) {
+            if (rt == 1 && at_t) { v1 = vb; i1 = ib; }
+            if (rb == 1 && at_b) { v1 = vt; i1 = it; }
+            if (rt == 2 && at_t) { v2 = vb; i2 = ib; }
+            if (rb == 2 && at_b) { v2 = vt; i2 = it; }
+            if (rt == 3 && at_t) { v3 = vb; i3 = ib; }
+            if (rb == 3 && at_b) { v3 = vt; i3 = it; }
         }
     }
-    for (uint32_t r = 0; r < 4; ++r) {
-        const uint32_t pos = c.lane + 64 * r;
-        if (pos < np) {
-            cval[pos] = v[r];
-            cid[pos] = id[r];
-        }
+    if (l < np) {
+        cval[l] = v0;
+        cid[l] = i0;
     }
+    if (R > 1) {
+        if (l + 64 < np) { cval[l + 64] = v1; cid[l + 64] = i1; }
+        if (l + 128 < np) { cval[l + 128] = v2; cid[l + 128] = i2; }
+        if (l + 192 < np) { cval[l + 192] = v3; cid[l + 192] = i3; }
+    }
+}
+
+PCG_DEV void partial_sort(const Ctx& c, uint32_t C, uint32_t np)
+{
+    if (C <= 64)
+        partial_sort_r<1>(c, C, np);
+    else
+        partial_sort_r<4>(c, C, np);
 }
 
 // Build the next path list after a branching leaf: duplicate (ptr rows + codeword
@@ -664,6 +719,7 @@ __global__ void __launch_bounds__(64) scl_kernel(KernelArgs a)
         for (uint32_t kop = 0; kop < a.nops; ++kop) {
             const uint32_t w = a.ops[kop];
             const uint32_t code = op_code(w), s = op_stage(w), o = op_off(w);
+            const uint64_t t0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
             switch (code) {
             case OP_F:
                 fg_dispatch<OP_F>(c, s, o, P, cur);
@@ -698,19 +754,21 @@ __global__ void __launch_bounds__(64) scl_kernel(KernelArgs a)
             }
             }
             wsync();
+            if (a.prof) {
+                const uint64_t t1 = __builtin_amdgcn_s_memtime();
+                if (c.lane == 0) {
+                    atomicAdd(&a.prof[2 * code], (unsigned long long)(t1 - t0));
+                    atomicAdd(&a.prof[2 * code + 1], 1ull);
+                }
+            }
         }
         // extractBestPath (scl_avx_float.cpp:711-750): first path in list order whose
         // detector check passes, else path 0.
         uint32_t* cwc = cw_tab(c, cur);
         if (!a.systematic) {
             // re-encode every path in place (G_N is applied per path)
-            const uint32_t M[5] = { 0x55555555u, 0x33333333u, 0x0F0F0F0Fu, 0x00FF00FFu, 0x0000FFFFu };
-            for (uint32_t e = c.lane; e < P * c.W; e += 64) {
-                uint32_t x = cwc[e];
-                for (uint32_t kk = 0, B = 1; kk < 5 && B < c.N; ++kk, B <<= 1)
-                    x ^= (x >> B) & M[kk];
-                cwc[e] = x;
-            }
+            for (uint32_t e = c.lane; e < P * c.W; e += 64)
+                cwc[e] = transform_word(cwc[e], c.N);
             wsync();
             for (uint32_t d = 1; d < c.W; d <<= 1) {
                 for (uint32_t e = c.lane; e < P * c.W; e += 64) {

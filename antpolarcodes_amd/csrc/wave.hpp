@@ -78,6 +78,18 @@ PCG_DEV void wave_argmax(float& v, uint32_t& i)
     }
 }
 
+// Polar transform stages B = 1..16 (B < N) inside one 32-bit word of packed bits:
+// x[i] ^= x[i + B] for positions with bit B clear (LSB-first packing).
+PCG_DEV uint32_t transform_word(uint32_t w, uint32_t N)
+{
+    if (N > 1) w ^= (w >> 1) & 0x55555555u;
+    if (N > 2) w ^= (w >> 2) & 0x33333333u;
+    if (N > 4) w ^= (w >> 4) & 0x0F0F0F0Fu;
+    if (N > 8) w ^= (w >> 8) & 0x00FF00FFu;
+    if (N > 16) w ^= (w >> 16) & 0x0000FFFFu;
+    return w;
+}
+
 // ---- packed codeword bits in LDS: position p -> word p>>5, bit p&31 ----------------
 PCG_DEV uint32_t get_bit(const uint32_t* w, uint32_t p) { return (w[p >> 5] >> (p & 31)) & 1u; }
 
@@ -98,6 +110,100 @@ PCG_DEV void put_bits(uint32_t* w, uint32_t o, uint32_t c, bool bit)
             w[o >> 5] = (old & ~msk) | (((uint32_t)m << sh) & msk);
         }
     }
+}
+
+} // namespace pcg
+
+namespace pcg {
+
+// ---- DPP / permlane butterflies (no LDS traffic) ------------------------------------
+// Partner of lane i at distance d in a butterfly over aligned groups of 2d lanes.
+// d = 1, 2: quad_perm xor; d = 4: row_half_mirror (i <-> 7-i); d = 8: row_mirror
+// (i <-> 15-i); d = 16: v_permlane16_swap; d = 32: v_permlane32_swap.  The mirror
+// partners are not xor partners, which is fine for commutative, idempotent combines
+// (min / max / argmin / argmax / xor-after-uniformity is NOT idempotent: see xor below).
+template <int D>
+PCG_DEV uint32_t bfly(uint32_t v)
+{
+    if constexpr (D == 1)
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false); // [1,0,3,2]
+    else if constexpr (D == 2)
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false); // [2,3,0,1]
+    else if constexpr (D == 4)
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xF, 0xF, false); // row_half_mirror
+    else if constexpr (D == 8)
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x140, 0xF, 0xF, false); // row_mirror
+    else if constexpr (D == 16) {
+        auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        return (lane_id() & 16) ? r[0] : r[1];
+    } else {
+        auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+        return (lane_id() & 32) ? r[0] : r[1];
+    }
+}
+
+PCG_DEV float bflyf(float v, int d)
+{
+    uint32_t u = fbits(v);
+    switch (d) {
+    case 1: u = bfly<1>(u); break;
+    case 2: u = bfly<2>(u); break;
+    case 4: u = bfly<4>(u); break;
+    case 8: u = bfly<8>(u); break;
+    case 16: u = bfly<16>(u); break;
+    default: u = bfly<32>(u); break;
+    }
+    return ubits(u);
+}
+
+PCG_DEV uint32_t bflyu(uint32_t u, int d)
+{
+    switch (d) {
+    case 1: return bfly<1>(u);
+    case 2: return bfly<2>(u);
+    case 4: return bfly<4>(u);
+    case 8: return bfly<8>(u);
+    case 16: return bfly<16>(u);
+    default: return bfly<32>(u);
+    }
+}
+
+// argmin over aligned groups of g lanes (g power of two <= 64); every lane of the
+// group ends with (min value, lowest index among equals).
+PCG_DEV void grp_argmin(float& v, uint32_t& i, uint32_t g)
+{
+    for (int d = 1; d < (int)g; d <<= 1) {
+        const float ov = bflyf(v, d);
+        const uint32_t oi = bflyu(i, d);
+        if (ov < v || (ov == v && oi < i)) {
+            v = ov;
+            i = oi;
+        }
+    }
+}
+
+// argmax over the whole wave: (max value, lowest index among equals); `i == ~0` marks
+// an empty lane that never wins.
+PCG_DEV void wave_argmax_dpp(float& v, uint32_t& i)
+{
+    for (int d = 1; d < 64; d <<= 1) {
+        const float ov = bflyf(v, d);
+        const uint32_t oi = bflyu(i, d);
+        if (oi != 0xffffffffu && (i == 0xffffffffu || ov > v || (ov == v && oi < i))) {
+            v = ov;
+            i = oi;
+        }
+    }
+}
+
+// XOR over aligned groups of g lanes.  Mirror partners are fine here too: after the
+// d-step every lane of a 2d-group holds the XOR of its d-group, so combining with any
+// lane of the other d-group is exact.
+PCG_DEV uint32_t grp_xor(uint32_t v, uint32_t g)
+{
+    for (int d = 1; d < (int)g; d <<= 1)
+        v ^= bflyu(v, d);
+    return v;
 }
 
 } // namespace pcg
