@@ -252,6 +252,8 @@ PCG_DEV float ordered_sum8(const Ctx& c, float s)
 }
 
 // ---- leaves --------------------------------------------------------------------------
+PCG_DEV void clear_bits(const Ctx& c, uint32_t s, uint32_t o, uint32_t P, uint32_t cur);
+
 // Rate-0 (scl_avx_float.cpp:316-337): metric += reduce_add(sum_lanes min(llr, +0)); no re-sort.
 template <typename Src>
 PCG_DEV void leaf_r0(const Ctx& c, Src src, uint32_t s, uint32_t o, uint32_t P, uint32_t cur)
@@ -275,7 +277,13 @@ PCG_DEV void leaf_r0(const Ctx& c, Src src, uint32_t s, uint32_t o, uint32_t P, 
         if (p < P && j == 0)
             met[p] = met[p] + pen;
     }
-    // bits = +INF -> 0
+    clear_bits(c, s, o, P, cur);
+}
+
+// bits [o, o+2^s) = 0 (+INF) for every path
+PCG_DEV void clear_bits(const Ctx& c, uint32_t s, uint32_t o, uint32_t P, uint32_t cur)
+{
+    const uint32_t n = 1u << s;
     uint32_t* cw = cw_tab(c, cur);
     if (n >= 32) {
         const uint32_t nw = n >> 5, lw = __builtin_ctz(nw);
@@ -436,6 +444,138 @@ PCG_DEV void weak_search(const Ctx& c, Src src, uint32_t s, uint32_t P, uint32_t
     }
 }
 
+// Lane-serial leaves for n <= 8 (the common case): lane p handles path p alone, in
+// registers, reproducing the reference's per-path loops literally.
+//   R0  : metric += reduce_add(0 + min(l_j, 0))                         :316-337
+//   REP : candidates m + reduce(0 + min(l,0)), m - reduce(0 + max(l,0)) :428-481
+//   R1/SPC: findWeakLlrs on |l| with its swaps, then the candidates     :353-413, 498-621
+PCG_DEV void load8(const float* x, uint32_t n, float (&v)[8])
+{
+    if (n >= 8) {
+        const float4 a = *reinterpret_cast<const float4*>(x);
+        const float4 b = *reinterpret_cast<const float4*>(x + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else if (n == 4) {
+        const float4 a = *reinterpret_cast<const float4*>(x);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+        v[4] = v[5] = v[6] = v[7] = 0.0f;
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            v[j] = j < (int)n ? x[j] : 0.0f;
+    }
+}
+
+PCG_DEV float ordered8(const float (&a)[8])
+{
+    return a[0] + a[1] + a[2] + a[3] + a[4] + a[5] + a[6] + a[7];
+}
+
+PCG_DEV void small_leaf(const Ctx& c, uint32_t code, uint32_t s, uint32_t P, uint32_t cur)
+{
+    const uint32_t n = 1u << s, p = c.lane;
+    if (p >= P)
+        return;
+    const uint8_t* ptr = ptr_tab(c, cur);
+    float* met = met_tab(c, cur);
+    const float* x = lds_stage(c, s).slot(ptr[p * 16 + s]);
+    float v[8];
+    load8(x, n, v);
+    const float m = met[p];
+    float* cval = c.lds + c.ly.cval;
+    if (code == OP_S_R0) {
+        float q[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            q[j] = 0.0f + minps(j < (int)n ? v[j] : 0.0f, 0.0f);
+        met[p] = m + ordered8(q);
+        return;
+    }
+    if (code == OP_S_REP) {
+        float z[8], o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float l = j < (int)n ? v[j] : 0.0f;
+            z[j] = 0.0f + minps(l, 0.0f);
+            o[j] = 0.0f + maxps(l, 0.0f);
+        }
+        cval[2 * p] = m + ordered8(z);
+        cval[2 * p + 1] = m - ordered8(o);
+        return;
+    }
+    // R1 / SPC
+    const uint32_t kk = code == OP_S_R1 ? 2 : 4;
+    float T[8];
+    uint32_t I[8];
+    uint32_t par = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        T[j] = fabs_(v[j]);
+        I[j] = (uint32_t)j;
+        if (j < (int)n)
+            par ^= fbits(v[j]);
+    }
+    const uint32_t lim = (n - 1) < kk ? (n - 1) : kk;
+    // Selection passes with the reference's swaps.  Element updates use bit masks
+    // instead of conditional array stores so the arrays stay in registers.
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        if (t < (int)lim) {
+            float bv = T[t];
+            uint32_t b = (uint32_t)t;
+#pragma unroll
+            for (int j = t + 1; j < 8; ++j) {
+                const bool better = j < (int)n && T[j] < bv;
+                bv = better ? T[j] : bv;
+                b = better ? (uint32_t)j : b;
+            }
+            const uint32_t tv = fbits(T[t]), ti = I[t];
+            uint32_t bi = I[t];
+#pragma unroll
+            for (int j = t + 1; j < 8; ++j) {
+                const uint32_t mj = 0u - (uint32_t)(b == (uint32_t)j);
+                bi = (I[j] & mj) | (bi & ~mj);
+                T[j] = ubits((tv & mj) | (fbits(T[j]) & ~mj));
+                I[j] = (ti & mj) | (I[j] & ~mj);
+            }
+            T[t] = bv;
+            I[t] = bi;
+        }
+    }
+    float* wk = c.lds + c.ly.wk;
+    uint32_t* wi = reinterpret_cast<uint32_t*>(c.lds + c.ly.wi);
+    uint32_t* wpar = reinterpret_cast<uint32_t*>(c.lds + c.ly.wpar);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        wk[p * 4 + t] = T[t];
+        wi[p * 4 + t] = I[t];
+    }
+    const uint32_t odd = par & 0x80000000u;
+    wpar[p] = odd;
+    if (code == OP_S_R1) {
+        cval[4 * p] = m;
+        cval[4 * p + 1] = m - T[0];
+        cval[4 * p + 2] = m - T[1];
+        cval[4 * p + 3] = m - T[0] - T[1];
+    } else {
+        float mm = m, pinv = 1.0f;
+        if (odd) {
+            pinv = 0.0f;
+            mm -= T[0];
+        }
+        float* cv = cval + 8 * p;
+        cv[0] = mm;
+        cv[1] = mm - pinv * T[0] - T[1];
+        cv[2] = mm - pinv * T[0] - T[2];
+        cv[3] = mm - pinv * T[0] - T[3];
+        cv[4] = mm - T[1] - T[2];
+        cv[5] = mm - T[1] - T[3];
+        cv[6] = mm - T[2] - T[3];
+        cv[7] = mm - pinv * T[0] - T[1] - T[2] - T[3];
+    }
+}
+
 // candidate metrics from the weak values (scl_avx_float.cpp:365-379 and :530-585)
 PCG_DEV void cand_r1_spc(const Ctx& c, uint32_t code, uint32_t P, uint32_t cur)
 {
@@ -572,12 +712,75 @@ PCG_DEV void partial_sort_r(const Ctx& c, uint32_t C, uint32_t np)
     }
 }
 
+// One bitonic compare-exchange of (value, id) with the exact xor-J partner; `keep_max`
+// says whether this lane keeps the larger value.
+template <int J>
+PCG_DEV void bitonic_cx(float& v, uint32_t& id, bool keep_max)
+{
+    const float ov = ubits(xpartner<J>(fbits(v)));
+    const uint32_t oi = xpartner<J>(id);
+    const bool take = keep_max ? (ov > v) : (ov < v);
+    if (take) {
+        v = ov;
+        id = oi;
+    }
+}
+
+template <int K, int J>
+PCG_DEV void bitonic_stage(float& v, uint32_t& id, uint32_t l)
+{
+    const bool desc = (K == 64) || ((l & K) == 0);
+    const bool lower = (l & J) == 0;
+    bitonic_cx<J>(v, id, lower == desc);
+}
+
+// Fast path for C <= 64 candidates: full bitonic sort (descending) across the wave.
+// When the np+1 leading values are pairwise distinct, swap-selection produces exactly
+// this order; otherwise (ties) the exact swap-selection simulation runs instead.
 PCG_DEV void partial_sort(const Ctx& c, uint32_t C, uint32_t np)
 {
-    if (C <= 64)
-        partial_sort_r<1>(c, C, np);
-    else
+    if (C > 64) {
         partial_sort_r<4>(c, C, np);
+        return;
+    }
+    float* cval = c.lds + c.ly.cval;
+    uint32_t* cid = reinterpret_cast<uint32_t*>(c.lds + c.ly.cid);
+    const uint32_t l = c.lane;
+    float v = l < C ? cval[l] : -__builtin_inff();
+    uint32_t id = l;
+    bitonic_stage<2, 1>(v, id, l);
+    bitonic_stage<4, 2>(v, id, l);
+    bitonic_stage<4, 1>(v, id, l);
+    bitonic_stage<8, 4>(v, id, l);
+    bitonic_stage<8, 2>(v, id, l);
+    bitonic_stage<8, 1>(v, id, l);
+    bitonic_stage<16, 8>(v, id, l);
+    bitonic_stage<16, 4>(v, id, l);
+    bitonic_stage<16, 2>(v, id, l);
+    bitonic_stage<16, 1>(v, id, l);
+    bitonic_stage<32, 16>(v, id, l);
+    bitonic_stage<32, 8>(v, id, l);
+    bitonic_stage<32, 4>(v, id, l);
+    bitonic_stage<32, 2>(v, id, l);
+    bitonic_stage<32, 1>(v, id, l);
+    bitonic_stage<64, 32>(v, id, l);
+    bitonic_stage<64, 16>(v, id, l);
+    bitonic_stage<64, 8>(v, id, l);
+    bitonic_stage<64, 4>(v, id, l);
+    bitonic_stage<64, 2>(v, id, l);
+    bitonic_stage<64, 1>(v, id, l);
+    // next lane's value (wave_shl:1 = lane i reads lane i+1)
+    const float vn = ubits((uint32_t)__builtin_amdgcn_update_dpp((int)fbits(v), (int)fbits(v), 0x130, 0xF, 0xF, false));
+    const uint32_t last = (np < C) ? np : (C - 1); // compare positions i, i+1 for i < last
+    const bool tie = (l < last) && (v == vn);
+    if (ballot(tie) != 0ull) {
+        partial_sort_r<1>(c, C, np);
+        return;
+    }
+    if (l < np) {
+        cval[l] = v;
+        cid[l] = id;
+    }
 }
 
 // Build the next path list after a branching leaf: duplicate (ptr rows + codeword
@@ -731,23 +934,45 @@ __global__ void __launch_bounds__(64) scl_kernel(KernelArgs a)
                 comb_op(c, s, o, P, cur);
                 break;
             case OP_S_R0:
-                with_src(c, s, [&](auto src) { leaf_r0(c, src, s, o, P, cur); });
+                if (s <= 3 && s < c.Sl && s != c.top) {
+                    small_leaf(c, OP_S_R0, s, P, cur);
+                    wsync();
+                    clear_bits(c, s, o, P, cur);
+                } else {
+                    with_src(c, s, [&](auto src) { leaf_r0(c, src, s, o, P, cur); });
+                }
                 break;
             default: { // branching leaves
                 const uint32_t k = code == OP_S_R1 ? 4 : code == OP_S_SPC ? 8 : 2;
-                if (code == OP_S_REP) {
+                auto stamp = [&](uint32_t ph, uint64_t& tp) {
+                    if (a.prof) {
+                        const uint64_t tn = __builtin_amdgcn_s_memtime();
+                        if (c.lane == 0)
+                            atomicAdd(&a.prof[2 * ph], (unsigned long long)(tn - tp));
+                        tp = tn;
+                    }
+                };
+                uint64_t tp = t0;
+                if (s <= 3 && s < c.Sl && s != c.top) {
+                    small_leaf(c, code, s, P, cur);
+                } else if (code == OP_S_REP) {
                     with_src(c, s, [&](auto src) { cand_rep(c, src, s, P, cur); });
                 } else {
                     with_src(c, s, [&](auto src) { weak_search(c, src, s, P, cur, code == OP_S_R1 ? 2 : 4); });
                     wsync();
+                    stamp(48, tp);
                     cand_r1_spc(c, code, P, cur);
                 }
                 wsync();
+                stamp(49, tp);
                 const uint32_t C = P * k;
                 const uint32_t np = C < c.L ? C : c.L;
                 partial_sort(c, C, np);
                 wsync();
+                stamp(50, tp);
                 with_src(c, s, [&](auto src) { branch_commit(c, src, code, s, o, P, np, k, cur); });
+                wsync();
+                stamp(51, tp);
                 cur ^= 1u;
                 P = np;
                 break;
@@ -808,7 +1033,7 @@ int scl_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* lds_
         return -4;
     const uint32_t top = (uint32_t)__builtin_ctz(N);
     // Largest LDS-resident stage set within the budget; the rest goes to global scratch.
-    uint32_t budget = 24 * 1024 / 4; // floats per wave (~6 codewords per CU)
+    uint32_t budget = 10 * 1024 / 4; // floats per wave (~16 codewords per CU)
     if (const char* e = getenv("PCG_SCL_LDS_KB"))
         budget = (uint32_t)atoi(e) * 1024 / 4;
     uint32_t Sl = top;

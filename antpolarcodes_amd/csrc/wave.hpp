@@ -142,43 +142,44 @@ PCG_DEV uint32_t bfly(uint32_t v)
     }
 }
 
-PCG_DEV float bflyf(float v, int d)
+template <int D>
+PCG_DEV float bflyf(float v)
 {
-    uint32_t u = fbits(v);
-    switch (d) {
-    case 1: u = bfly<1>(u); break;
-    case 2: u = bfly<2>(u); break;
-    case 4: u = bfly<4>(u); break;
-    case 8: u = bfly<8>(u); break;
-    case 16: u = bfly<16>(u); break;
-    default: u = bfly<32>(u); break;
-    }
-    return ubits(u);
+    return ubits(bfly<D>(fbits(v)));
 }
 
-PCG_DEV uint32_t bflyu(uint32_t u, int d)
+template <int D>
+PCG_DEV void argmin_step(float& v, uint32_t& i)
 {
-    switch (d) {
-    case 1: return bfly<1>(u);
-    case 2: return bfly<2>(u);
-    case 4: return bfly<4>(u);
-    case 8: return bfly<8>(u);
-    case 16: return bfly<16>(u);
-    default: return bfly<32>(u);
+    const float ov = bflyf<D>(v);
+    const uint32_t oi = bfly<D>(i);
+    if (ov < v || (ov == v && oi < i)) {
+        v = ov;
+        i = oi;
     }
 }
 
 // argmin over aligned groups of g lanes (g power of two <= 64); every lane of the
-// group ends with (min value, lowest index among equals).
+// group ends with (min value, lowest index among equals).  Each level is a
+// compile-time DPP/permlane op behind one uniform branch.
 PCG_DEV void grp_argmin(float& v, uint32_t& i, uint32_t g)
 {
-    for (int d = 1; d < (int)g; d <<= 1) {
-        const float ov = bflyf(v, d);
-        const uint32_t oi = bflyu(i, d);
-        if (ov < v || (ov == v && oi < i)) {
-            v = ov;
-            i = oi;
-        }
+    if (g > 1) argmin_step<1>(v, i);
+    if (g > 2) argmin_step<2>(v, i);
+    if (g > 4) argmin_step<4>(v, i);
+    if (g > 8) argmin_step<8>(v, i);
+    if (g > 16) argmin_step<16>(v, i);
+    if (g > 32) argmin_step<32>(v, i);
+}
+
+template <int D>
+PCG_DEV void argmax_step(float& v, uint32_t& i)
+{
+    const float ov = bflyf<D>(v);
+    const uint32_t oi = bfly<D>(i);
+    if (oi != 0xffffffffu && (i == 0xffffffffu || ov > v || (ov == v && oi < i))) {
+        v = ov;
+        i = oi;
     }
 }
 
@@ -186,23 +187,43 @@ PCG_DEV void grp_argmin(float& v, uint32_t& i, uint32_t g)
 // an empty lane that never wins.
 PCG_DEV void wave_argmax_dpp(float& v, uint32_t& i)
 {
-    for (int d = 1; d < 64; d <<= 1) {
-        const float ov = bflyf(v, d);
-        const uint32_t oi = bflyu(i, d);
-        if (oi != 0xffffffffu && (i == 0xffffffffu || ov > v || (ov == v && oi < i))) {
-            v = ov;
-            i = oi;
-        }
-    }
+    argmax_step<1>(v, i);
+    argmax_step<2>(v, i);
+    argmax_step<4>(v, i);
+    argmax_step<8>(v, i);
+    argmax_step<16>(v, i);
+    argmax_step<32>(v, i);
 }
 
-// XOR over aligned groups of g lanes.  Mirror partners are fine here too: after the
-// d-step every lane of a 2d-group holds the XOR of its d-group, so combining with any
-// lane of the other d-group is exact.
+// Exact xor partner: value of lane (i ^ J) for J in {1,2,4,8,16,32}.
+template <int J>
+PCG_DEV uint32_t xpartner(uint32_t v)
+{
+    if constexpr (J == 1)
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false);
+    else if constexpr (J == 2)
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false);
+    else if constexpr (J == 4) {
+        // lanes with bit 2 clear read lane i+4 (row_shl:4), the others lane i-4 (row_shr:4)
+        const uint32_t up = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x104, 0xF, 0xF, false);
+        const uint32_t dn = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x114, 0xF, 0xF, false);
+        return (lane_id() & 4) ? dn : up;
+    } else if constexpr (J == 8)
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x128, 0xF, 0xF, false); // row_ror:8
+    else
+        return bfly<J>(v); // permlane16/32 swaps are exact xor partners
+}
+
+// XOR over aligned groups of g lanes.  Mirror partners are fine: after the d-step
+// every lane of a 2d-group holds the XOR of its d-group.
 PCG_DEV uint32_t grp_xor(uint32_t v, uint32_t g)
 {
-    for (int d = 1; d < (int)g; d <<= 1)
-        v ^= bflyu(v, d);
+    if (g > 1) v ^= bfly<1>(v);
+    if (g > 2) v ^= bfly<2>(v);
+    if (g > 4) v ^= bfly<4>(v);
+    if (g > 8) v ^= bfly<8>(v);
+    if (g > 16) v ^= bfly<16>(v);
+    if (g > 32) v ^= bfly<32>(v);
     return v;
 }
 
