@@ -451,20 +451,18 @@ PCG_DEV void weak_search(const Ctx& c, Src src, uint32_t s, uint32_t P, uint32_t
 //   R1/SPC: findWeakLlrs on |l| with its swaps, then the candidates     :353-413, 498-621
 PCG_DEV void load8(const float* x, uint32_t n, float (&v)[8])
 {
-    if (n >= 8) {
-        const float4 a = *reinterpret_cast<const float4*>(x);
-        const float4 b = *reinterpret_cast<const float4*>(x + 4);
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-        v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-    } else if (n == 4) {
-        const float4 a = *reinterpret_cast<const float4*>(x);
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-        v[4] = v[5] = v[6] = v[7] = 0.0f;
-    } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            v[j] = j < (int)n ? x[j] : 0.0f;
+    // slots are 16-byte aligned and at least 4 floats wide (lds_stage_base)
+    const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float4 a = *reinterpret_cast<const float4*>(x);
+    const float4 b = n >= 8 ? *reinterpret_cast<const float4*>(x + 4) : z4;
+    if (n < 4) {
+        a.z = 0.0f;
+        a.w = 0.0f;
+        if (n < 2)
+            a.y = 0.0f;
     }
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
 PCG_DEV float ordered8(const float (&a)[8])
