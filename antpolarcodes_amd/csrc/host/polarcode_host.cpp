@@ -1,0 +1,331 @@
+// polarcode_host.cpp -- host C++ library (libpolarcode_amd.so) mirroring the
+// reference's PolarCode::{ErrorDetection, Construction, Encoding, Decoding} API on
+// top of the C ABI (include/pcg.h).  No device code here.
+#include <polarcode/construction/constructor.h>
+#include <polarcode/decoding/decoder.h>
+#include <polarcode/encoding/encoder.h>
+#include <polarcode/errordetection/errordetector.h>
+
+#include "../crc_host.hpp"
+#include <pcg.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <stdexcept>
+
+namespace PolarCode {
+
+// =============================================================== ErrorDetection
+namespace ErrorDetection {
+
+Dummy globalDummyDetector;
+
+void Crc::generate(void* data, int bytes) { pcg::crc_generate((int)mBits, static_cast<uint8_t*>(data), bytes); }
+
+bool Crc::check(void* data, int bytes) { return pcg::crc_check((int)mBits, static_cast<uint8_t*>(data), bytes); }
+
+int Crc::multiCheck(void** data, int nArrays, int nBytes)
+{
+    for (int a = 0; a < nArrays; ++a)
+        if (check(data[a], nBytes))
+            return a;
+    return -1;
+}
+
+Detector* create(unsigned size, std::string type)
+{
+    std::transform(type.begin(), type.end(), type.begin(), [](unsigned char c) { return std::tolower(c); });
+    if (type.find("crc") != std::string::npos) {
+        switch (size) {
+        case 0:
+            return new Dummy();
+        case 8:
+            return new CRC8();
+        case 16:
+            return new CRC16();
+        case 32:
+            return new CRC32();
+        default:
+            throw std::logic_error("CRC INVALID SIZE!");
+        }
+    }
+    if (type.find("cmac") != std::string::npos)
+        throw std::logic_error("CMAC detectors are not part of this build");
+    throw std::runtime_error("Unknown Error detector requested!");
+}
+
+int gpuKind(Detector* d)
+{
+    if (!d)
+        return 0;
+    const std::string t = d->getType();
+    if (t == "DUMMY")
+        return 0;
+    if (t == "CRC") {
+        const unsigned b = d->getCheckBitCount();
+        if (b == 0 || b == 8 || b == 16 || b == 32)
+            return (int)b;
+    }
+    return -1;
+}
+
+} // namespace ErrorDetection
+
+// =============================================================== Construction
+namespace Construction {
+
+std::vector<unsigned> frozen_bits(const int blockLength,
+                                  const int infoLength,
+                                  const float designSNR,
+                                  const std::string& constructor_type)
+{
+    std::string t = constructor_type;
+    std::transform(t.begin(), t.end(), t.begin(), [](unsigned char c) { return std::tolower(c); });
+    if (t.find("be") != std::string::npos || t.find("5g") != std::string::npos)
+        throw std::logic_error("construction '" + constructor_type + "' is not part of this build");
+    const int N = blockLength, K = infoLength;
+    if (N < 1 || (N & (N - 1)) || K < 0 || K > N)
+        throw std::invalid_argument("block length must be a power of two and 0 <= K <= N");
+    // Bhattacharyya bounds, bhattacharrya.cpp:39-82
+    const float lin = (float)std::pow(10.0, designSNR / 10.0);
+    const float init = (float)std::exp(-2.0 * lin * K / N);
+    std::vector<double> z(N);
+    z[0] = init;
+    for (int stage = (int)std::log2(N) - 1; stage >= 0; --stage) {
+        const int B = 1 << stage;
+        for (int j = 0; j < N; j += 2 * B) {
+            const double T = z[j];
+            z[j + B] = T * T;
+            z[j] = 2 * T - z[j + B];
+        }
+    }
+    std::vector<int> perm(N);
+    for (int i = 0; i < N; ++i)
+        perm[i] = i;
+    std::stable_sort(perm.begin(), perm.end(), [&](int a, int b) { return z[a] > z[b]; });
+    std::vector<unsigned> f(perm.begin(), perm.begin() + (N - K));
+    std::sort(f.begin(), f.end());
+    return f;
+}
+
+} // namespace Construction
+
+// =============================================================== Encoding
+namespace Encoding {
+
+Encoder::Encoder() : mErrorDetector(&ErrorDetection::globalDummyDetector), mBlockLength(0), mSystematic(true) {}
+
+ButterflyFipPacked::ButterflyFipPacked(size_t blockLength, const std::vector<unsigned>& frozenBits)
+{
+    initialize(blockLength, frozenBits);
+}
+
+void ButterflyFipPacked::initialize(size_t blockLength, const std::vector<unsigned>& frozenBits)
+{
+    mBlockLength = blockLength;
+    mFrozenBits.assign(frozenBits.begin(), frozenBits.end());
+    mIsFrozen.assign(blockLength, 0);
+    for (unsigned v : mFrozenBits)
+        if (v < blockLength)
+            mIsFrozen[v] = 1;
+}
+
+static void transform(std::vector<uint8_t>& x)
+{
+    const size_t N = x.size();
+    for (size_t B = 1; B < N; B <<= 1)
+        for (size_t j = 0; j < N; j += 2 * B)
+            for (size_t i = j; i < j + B; ++i)
+                x[i] ^= x[i + B];
+}
+
+void ButterflyFipPacked::encode_vector(void* pInfo, void* pCode)
+{
+    const size_t N = mBlockLength, K = infoLength();
+    std::vector<uint8_t> d(static_cast<uint8_t*>(pInfo), static_cast<uint8_t*>(pInfo) + (K + 7) / 8);
+    mErrorDetector->generate(d.data(), (int)(K / 8)); // butterfly_fip_packed.cpp:47-48
+    std::memcpy(pInfo, d.data(), d.size());
+    std::vector<uint8_t> u(N, 0);
+    for (size_t i = 0, j = 0; i < N; ++i)
+        if (!mIsFrozen[i]) {
+            u[i] = (d[j / 8] >> (7 - j % 8)) & 1u;
+            ++j;
+        }
+    transform(u);
+    if (mSystematic) {
+        for (size_t i = 0; i < N; ++i)
+            if (mIsFrozen[i])
+                u[i] = 0;
+        transform(u);
+    }
+    uint8_t* c = static_cast<uint8_t*>(pCode);
+    std::memset(c, 0, N / 8);
+    for (size_t i = 0; i < N; ++i)
+        if (u[i])
+            c[i / 8] |= (uint8_t)(0x80u >> (i % 8));
+}
+
+} // namespace Encoding
+
+// =============================================================== Decoding
+namespace Decoding {
+
+Decoder::Decoder() : mErrorDetector(&ErrorDetection::globalDummyDetector) {}
+
+Decoder::~Decoder() {}
+
+void Decoder::initialize(size_t blockLength, const std::vector<unsigned>& frozenBits)
+{
+    mBlockLength = blockLength;
+    mFrozenBits.assign(frozenBits.begin(), frozenBits.end());
+    mLlr.assign(blockLength, 0.0f);
+    mOutputContainer.assign((blockLength - frozenBits.size() + 7) / 8 + 1, 0);
+}
+
+void Decoder::setSystematic(bool sys) { mSystematic = sys; }
+
+void Decoder::setErrorDetection(ErrorDetection::Detector* pDetector) { mErrorDetector = pDetector; }
+
+void Decoder::setSignal(const float* pLlr) { std::memcpy(mLlr.data(), pLlr, 4 * mBlockLength); }
+
+void Decoder::getDecodedInformationBits(void* pData)
+{
+    std::memcpy(pData, mOutputContainer.data(), (mBlockLength - mFrozenBits.size() + 7) / 8);
+}
+
+bool Decoder::decode_vector(const float* pLlr, void* pData)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    setSignal(pLlr);
+    const bool r = decode();
+    getDecodedInformationBits(pData);
+    mDecoderDuration = (size_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                           std::chrono::steady_clock::now() - t0)
+                           .count();
+    return r;
+}
+
+static void throw_pcg(int rc)
+{
+    const std::string msg = pcg_last_error();
+    if (rc == PCG_E_FROZEN)
+        throw std::invalid_argument(msg);
+    if (rc == PCG_E_ARG)
+        throw std::logic_error(msg);
+    throw std::runtime_error("pcg error " + std::to_string(rc) + ": " + msg);
+}
+
+GpuDecoder::GpuDecoder(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits, int device)
+    : mListSize(listSize), mDevice(device)
+{
+    initialize(blockLength, frozenBits);
+}
+
+GpuDecoder::~GpuDecoder() { releasePlan(); }
+
+void GpuDecoder::releasePlan()
+{
+    if (mPlan)
+        pcg_plan_destroy(mPlan);
+    mPlan = nullptr;
+}
+
+void GpuDecoder::initialize(size_t blockLength, const std::vector<unsigned>& frozenBits)
+{
+    Decoder::initialize(blockLength, frozenBits);
+    releasePlan();
+    // validate (and classify) now so invalid codes fail at construction like the reference
+    pcg_plan* probe = nullptr;
+    const int rc = pcg_plan_create(&probe, (uint32_t)blockLength, (uint32_t)mListSize, mFrozenBits.data(),
+                                   (uint32_t)mFrozenBits.size(), 1, 0, -1);
+    if (rc != 0)
+        throw_pcg(rc);
+    pcg_plan_destroy(probe);
+}
+
+void GpuDecoder::setSystematic(bool sys) { mSystematic = sys; }
+
+void GpuDecoder::setErrorDetection(ErrorDetection::Detector* pDetector)
+{
+    if (ErrorDetection::gpuKind(pDetector) < 0)
+        throw std::logic_error("detector " + pDetector->getType() + " cannot be evaluated on the GPU");
+    mErrorDetector = pDetector;
+}
+
+void GpuDecoder::ensurePlan()
+{
+    const int kind = ErrorDetection::gpuKind(mErrorDetector);
+    if (mPlan && kind == mPlanKind && mSystematic == mPlanSys)
+        return;
+    releasePlan();
+    const int rc = pcg_plan_create(&mPlan, (uint32_t)mBlockLength, (uint32_t)mListSize, mFrozenBits.data(),
+                                   (uint32_t)mFrozenBits.size(), mSystematic ? 1 : 0, kind, mDevice);
+    if (rc != 0) {
+        mPlan = nullptr;
+        throw_pcg(rc);
+    }
+    mPlanKind = kind;
+    mPlanSys = mSystematic;
+}
+
+bool GpuDecoder::decode()
+{
+    uint8_t ok = 0;
+    decodeBatch(mLlr.data(), 1, mOutputContainer.data(), &ok, nullptr);
+    mLastOk = ok != 0;
+    return mLastOk;
+}
+
+bool GpuDecoder::decodeBatch(const float* llr, size_t F, uint8_t* info, uint8_t* ok, float* metrics)
+{
+    ensurePlan();
+    std::vector<uint8_t> okv;
+    uint8_t* okp = ok;
+    if (!okp) {
+        okv.assign(F, 0);
+        okp = okv.data();
+    }
+    const int rc = pcg_decode_f32_host(mPlan, llr, F, info, okp, mListSize > 1 ? metrics : nullptr);
+    if (rc != 0)
+        throw_pcg(rc);
+    for (size_t f = 0; f < F; ++f)
+        if (!okp[f])
+            return false;
+    return true;
+}
+
+void GpuDecoder::decodeBatchDevice(const float* llr, size_t F, uint8_t* info, uint8_t* ok, float* metrics,
+                                   void* hipStream)
+{
+    ensurePlan();
+    const int rc = pcg_decode_f32(mPlan, llr, F, info, ok, mListSize > 1 ? metrics : nullptr, hipStream);
+    if (rc != 0)
+        throw_pcg(rc);
+}
+
+Decoder* makeDecoder(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits, int)
+{
+    Decoder* dec;
+    if (listSize <= 1)
+        dec = new GpuFastSscFloat(blockLength, frozenBits);
+    else
+        dec = new GpuSclFloat(blockLength, listSize, frozenBits);
+    dec->setErrorDetection(new ErrorDetection::CRC8()); // decoder.cpp:85 (never freed there either)
+    return dec;
+}
+
+Decoder* create(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits, std::string type)
+{
+    std::transform(type.begin(), type.end(), type.begin(), [](unsigned char c) { return std::tolower(c); });
+    if (type.find("gpu") != std::string::npos || type.find("float") != std::string::npos)
+        return makeDecoder(blockLength, listSize, frozenBits, 1);
+    if (type.find("char") != std::string::npos || type.find("mixed") != std::string::npos ||
+        type.find("scan") != std::string::npos)
+        throw std::logic_error("PolarDecoder type '" + type + "' is not part of this build (use \"gpu\")");
+    throw std::logic_error("Unknown PolarDecoder type!");
+}
+
+} // namespace Decoding
+} // namespace PolarCode

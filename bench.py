@@ -126,11 +126,10 @@ def main():
     fer = float(np.mean(~(dec == info).all(axis=1)))
     ok_rate = float(d_ok.float().mean().item())
 
-    t = torch.tensor([wall], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max = float(t.item())
-    total_frames = F * args.steps * world
+    from antpolarcodes_amd.distributed import reduce_stats
+    st = reduce_stats({"wall": (wall, "max"), "frames": (F * args.steps, "sum")})
+    wall_max = st["wall"]
+    total_frames = int(st["frames"])
     value = total_frames / wall_max
 
     if rank == 0:

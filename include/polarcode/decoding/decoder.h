@@ -1,0 +1,138 @@
+/* -*- c++ -*- */
+// PolarCode::Decoding -- drop-in for the reference's decoder interface
+// (include/polarcode/decoding/decoder.h:40-211 of david13pod/antPolarCodes).
+//
+// The virtual base keeps the reference's names, argument meanings and error
+// behaviour; the implementations (GpuFastSscFloat, GpuSclFloat) run the
+// MI355X kernels through the C ABI of include/pcg.h.  New: decodeBatch() for F
+// frames per call (host buffers) and decodeBatchDevice() (device buffers,
+// asynchronous on a HIP stream).
+#ifndef PCA_DECODER_H
+#define PCA_DECODER_H
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include <polarcode/errordetection/errordetector.h>
+
+struct pcg_plan;
+
+namespace PolarCode {
+namespace Decoding {
+
+class Decoder
+{
+protected:
+    size_t mDecoderDuration = 0;
+    ErrorDetection::Detector* mErrorDetector; ///< not owned (as in the reference)
+    size_t mBlockLength = 0;
+    bool mSystematic = true;
+    std::vector<unsigned> mFrozenBits;
+    std::vector<float> mLlr;                  ///< setSignal() input (one frame)
+    std::vector<unsigned char> mOutputContainer;
+    bool mLastOk = false;
+
+public:
+    Decoder();
+    virtual ~Decoder();
+
+    /// Decode the frame given by setSignal(); returns the detector's verdict.
+    virtual bool decode() = 0;
+    /// setSignal + decode + getDecodedInformationBits (decoder.cpp:154-167).
+    bool decode_vector(const float* pLlr, void* pData);
+    size_t duration_ns() { return mDecoderDuration; }
+
+    virtual void initialize(size_t blockLength, const std::vector<unsigned>& frozenBits);
+    std::vector<unsigned> frozenBits() { return mFrozenBits; }
+    size_t blockLength() { return mBlockLength; }
+    size_t infoLength() { return mBlockLength - mFrozenBits.size(); }
+    unsigned char* packedOutput() { return mOutputContainer.data(); }
+
+    virtual void setSystematic(bool sys);
+    bool isSystematic() { return mSystematic; }
+    virtual void setErrorDetection(ErrorDetection::Detector* pDetector);
+    std::string getErrorDetectionMode()
+    {
+        return mErrorDetector->getType() + "-" + std::to_string(mErrorDetector->getCheckBitCount());
+    }
+    virtual size_t getListSize() { return 1; }
+    virtual void setSignal(const float* pLlr);
+    void getDecodedInformationBits(void* pData);
+
+    /// Batched decode of F frames (host memory): llr F x N, info F x ceil(K/8),
+    /// ok F (nullable), metrics F x L (nullable, SCL only).  Returns true if every
+    /// frame passed the detector.
+    virtual bool decodeBatch(const float* llr, size_t F, uint8_t* info, uint8_t* ok = nullptr,
+                             float* metrics = nullptr) = 0;
+    /// Same with device pointers, asynchronous on `hipStream` (null = default stream).
+    virtual void decodeBatchDevice(const float* llr, size_t F, uint8_t* info, uint8_t* ok = nullptr,
+                                   float* metrics = nullptr, void* hipStream = nullptr) = 0;
+};
+
+/// Shared GPU plumbing: owns one pcg_plan, rebuilt when code / detector / systematic
+/// flag change.
+class GpuDecoder : public Decoder
+{
+protected:
+    size_t mListSize;
+    int mDevice;
+    pcg_plan* mPlan = nullptr;
+    int mPlanKind = -2;
+    bool mPlanSys = true;
+    void ensurePlan();
+    void releasePlan();
+
+public:
+    GpuDecoder(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits, int device);
+    ~GpuDecoder() override;
+    bool decode() override;
+    void initialize(size_t blockLength, const std::vector<unsigned>& frozenBits) override;
+    void setSystematic(bool sys) override;
+    void setErrorDetection(ErrorDetection::Detector* pDetector) override;
+    size_t getListSize() override { return mListSize; }
+    bool decodeBatch(const float* llr, size_t F, uint8_t* info, uint8_t* ok = nullptr,
+                     float* metrics = nullptr) override;
+    void decodeBatchDevice(const float* llr, size_t F, uint8_t* info, uint8_t* ok = nullptr,
+                           float* metrics = nullptr, void* hipStream = nullptr) override;
+    int device() const { return mDevice; }
+};
+
+/// Fast-SSC (FastSscAvxFloat, fastssc_avx_float.cpp) on the GPU.
+class GpuFastSscFloat : public GpuDecoder
+{
+public:
+    GpuFastSscFloat(size_t blockLength, const std::vector<unsigned>& frozenBits, int device = 0)
+        : GpuDecoder(blockLength, 1, frozenBits, device)
+    {
+    }
+};
+
+/// CRC-aided SCL (SclAvxFloat, scl_avx_float.cpp) on the GPU; listSize 2..32.
+class GpuSclFloat : public GpuDecoder
+{
+public:
+    GpuSclFloat(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,
+                int device = 0)
+        : GpuDecoder(blockLength, listSize, frozenBits, device)
+    {
+    }
+};
+
+/// makeDecoder (decoder.cpp:54-87): L == 1 -> Fast-SSC, else SCL; always installs
+/// a CRC-8 detector (the reference's Q5 behaviour).
+Decoder* makeDecoder(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,
+                     int decoder_impl = 1);
+
+/// create (decoder.cpp:26-52).  "gpu" and "float" select the MI355X float decoders
+/// (listSize < 2 -> Fast-SSC).  "char", "mixed" and "scan" are reference decoders
+/// outside this build and raise std::logic_error; unknown strings raise
+/// std::logic_error("Unknown PolarDecoder type!") exactly as the reference.
+Decoder* create(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,
+                std::string decoderType);
+
+} // namespace Decoding
+} // namespace PolarCode
+
+#endif

@@ -1068,3 +1068,22 @@ double orc_bench(uint32_t N, uint32_t L, const uint32_t* frozen, uint32_t nf,
     double s = (b.tv_sec - a.tv_sec) + 1e-9 * (b.tv_nsec - a.tv_nsec);
     return (double)F * reps / s;
 }
+
+/* KAT hooks: the reference's 8-lane F / G / CombineBitsShort on plain arrays
+ * (test/polarcode/decodingtest.cpp:462-494 exercises these). */
+void orc_f(const float* in, float* out, uint32_t h)
+{
+    for (uint32_t i = 0; i < h; ++i) out[i] = polar_f(in[i], in[h + i]);
+}
+void orc_g(const float* in, const float* bits, float* out, uint32_t h)
+{
+    for (uint32_t i = 0; i < h; ++i) out[i] = polar_g(in[i], in[h + i], bits[i]);
+}
+void orc_combine_short(const float* l, const float* r, float* out, uint32_t h)
+{
+    for (uint32_t i = 0; i < 8; ++i) out[i] = 0.0f;
+    for (uint32_t i = 0; i < h; ++i) {
+        out[i] = fxor(l[i], r[i]);
+        out[h + i] = r[i];
+    }
+}

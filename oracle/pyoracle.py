@@ -45,7 +45,30 @@ class Oracle:
         lib.orc_frozen_bits_bb.argtypes = [_U32, _U32, C.c_float, _P]
         lib.orc_bench.argtypes = [_U32, _U32, _P, _U32, _P, _U64, _I]
         lib.orc_bench.restype = C.c_double
+        lib.orc_f.argtypes = [_P, _P, _U32]
+        lib.orc_g.argtypes = [_P, _P, _P, _U32]
+        lib.orc_combine_short.argtypes = [_P, _P, _P, _U32]
         self.lib = lib
+
+    def f(self, left, right):
+        x = np.ascontiguousarray(np.concatenate([left, right]), np.float32)
+        out = np.zeros(len(left), np.float32)
+        self.lib.orc_f(_p(x), _p(out), len(left))
+        return out
+
+    def g(self, left, right, bits):
+        x = np.ascontiguousarray(np.concatenate([left, right]), np.float32)
+        b = np.ascontiguousarray(bits, np.float32)
+        out = np.zeros(len(left), np.float32)
+        self.lib.orc_g(_p(x), _p(b), _p(out), len(left))
+        return out
+
+    def combine_short(self, left, right, h):
+        l8 = np.ascontiguousarray(left, np.float32)
+        r8 = np.ascontiguousarray(right, np.float32)
+        out = np.zeros(8, np.float32)
+        self.lib.orc_combine_short(_p(l8), _p(r8), _p(out), h)
+        return out
 
     def sc_decode(self, N, frozen, llr, systematic=True, crc=-1, soft=False):
         fr = _frozen(frozen)
