@@ -3,6 +3,7 @@
 
 #include "crc_host.hpp"
 
+#include <cstdlib>
 #include <random>
 
 namespace pcg {
@@ -123,6 +124,24 @@ void sc_emit(PlanHost& p, const std::vector<uint32_t>& f, uint32_t n, uint32_t o
     p.ops.push_back(mkop(OP_COMB, n, off));
 }
 
+// SCL classification of a small node (n <= 4) as an ST8 descriptor kind.
+uint32_t scl_small_kind(const std::vector<uint32_t>& f, uint32_t n, PlanHost& p, uint32_t* sub)
+{
+    const uint32_t nf = (uint32_t)f.size();
+    p.node_count++;
+    if (nf == 0) return ST_R1;
+    if (nf == n) return ST_R0;
+    if (nf == n - 1 && n < 8) return ST_REP;
+    if (nf == 1) return ST_SPC;
+    // ShortRateRNode (n == 4): two size-2 children (R0 / R1 / Rep only)
+    std::vector<uint32_t> lf, rf;
+    split(f, n / 2, lf, rf);
+    uint32_t d0 = 0, d1 = 0;
+    const uint32_t k0 = scl_small_kind(lf, n / 2, p, &d0), k1 = scl_small_kind(rf, n / 2, p, &d1);
+    *sub = k0 | (k1 << 2);
+    return ST_RATER;
+}
+
 // SclAvx::createDecoder (scl_avx_float.cpp:624-651), RateRNode::decode order (:229-263).
 void scl_emit(PlanHost& p, const std::vector<uint32_t>& f, uint32_t n, uint32_t off)
 {
@@ -140,6 +159,17 @@ void scl_emit(PlanHost& p, const std::vector<uint32_t>& f, uint32_t n, uint32_t 
     std::vector<uint32_t> lf, rf;
     split(f, h, lf, rf);
     p.node_types.push_back(0);
+    if (n == 8 && p.scl_st8) { // ShortRateRNode of size 8: one lane-serial subtree op
+        uint32_t desc = 0;
+        for (uint32_t c = 0; c < 2; ++c) {
+            uint32_t sub = 0;
+            const uint32_t kind = scl_small_kind(c ? rf : lf, 4, p, &sub);
+            desc |= (kind | (sub << 3)) << (8 * c);
+        }
+        p.ops.push_back(mkop(OP_S_ST8, n, off));
+        p.ops.push_back(desc);
+        return;
+    }
     p.ops.push_back(mkop(OP_F, n, off));
     scl_emit(p, lf, h, off);
     p.ops.push_back(mkop(OP_G, n, off));
@@ -188,6 +218,7 @@ int build_plan(PlanHost& p,
     p.systematic = systematic ? 1 : 0;
     p.crc_kind = crc_kind;
     p.frozen.assign(frozen, frozen + nf);
+    p.scl_st8 = L <= 8 && getenv("PCG_SCL_NO_ST8") == nullptr; // ST8 sorts <= 64 candidates
     try {
         if (L == 1)
             sc_emit(p, p.frozen, N, 0);

@@ -46,7 +46,15 @@ enum OpCode : uint32_t {
     OP_S_R1 = 41,  // :353-413
     OP_S_REP = 42, // :428-481
     OP_S_SPC = 43, // :498-621
+    // A whole size-8 SCL subtree run lane-serially (lane = path) in registers; the
+    // next schedule word is its descriptor (see scl_emit in plan.cpp).
+    OP_S_ST8 = 44,
 };
+
+// ST8 descriptor: per size-4 child c (c = 0 left, 1 right) at bits 8c..8c+6:
+// [0..2] kind (ST_R0, ST_R1, ST_REP, ST_SPC, ST_RATER), [3..4] / [5..6] kinds of its
+// size-2 children when it is a RateR (ST_R0, ST_R1, ST_REP).
+enum StKind : uint32_t { ST_R0 = 0, ST_R1 = 1, ST_REP = 2, ST_SPC = 3, ST_RATER = 4 };
 
 PCG_HD inline uint32_t op_code(uint32_t w) { return w & 0xffu; }
 PCG_HD inline uint32_t op_stage(uint32_t w) { return (w >> 8) & 0xffu; }
@@ -63,6 +71,7 @@ struct PlanHost {
     uint32_t crc_c0 = 0;            // syndrome of the all-zero message
     uint32_t node_count = 0;
     std::vector<int> node_types;    // pre-order census (op code of each node; 0 = internal)
+    bool scl_st8 = true;            // emit lane-serial size-8 subtrees for SCL
 };
 
 // Returns 0, or a negative pcg.h error code with *err set.

@@ -884,6 +884,260 @@ PCG_DEV void write_bits_from_info(const Ctx& c, const KernelArgs& a, const uint3
     *syn = wave_xor(sv) ^ a.crc_c0;
 }
 
+// ======================= ST8: a size-8 subtree, lane = path, in registers ==========
+// Runs RateR(8) -> {R0, R1, Rep, SPC, RateR(4) -> {R0, R1, Rep}} exactly as the
+// reference's ShortRateRNode recursion (scl_avx_float.cpp:273-307) and leaves
+// (:316-621) for every path at once, keeping the size-8 input, the size-4 input and
+// the 8 codeword bits of each path in its lane's registers.  A branching leaf
+// gathers the candidates, runs the same exact selection as the other leaves and
+// moves the survivors' register state with ds_bpermute; the LDS path state
+// (codeword prefix, slot table) is duplicated once, at the end of the subtree, from
+// the path each survivor descends from.
+struct St8 {
+    float x8[8];
+    float a4[4];
+    uint32_t bits; // bit i = codeword position o + i
+    uint32_t root; // path index at subtree entry
+    float m;
+    uint32_t P;
+    bool branched;
+};
+
+// lane-serial candidates of a leaf of size n (2 or 4) on v[0..n): values cv[0..k) and
+// per-candidate n-bit patterns packed 4 bits each into pat.
+PCG_DEV void st_cands(uint32_t kind, const float (&v)[4], uint32_t n, float m, float (&cv)[8], uint32_t& pat)
+{
+    const uint32_t nmask = (1u << n) - 1u;
+    if (kind == ST_REP) { // :428-481 (zero padded to 8 lanes)
+        float z[8], o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float l = j < (int)n && j < 4 ? v[j & 3] : 0.0f;
+            z[j] = 0.0f + minps(l, 0.0f);
+            o[j] = 0.0f + maxps(l, 0.0f);
+        }
+        cv[0] = m + ordered8(z);
+        cv[1] = m - ordered8(o);
+        pat = nmask << 4;
+        return;
+    }
+    float T[4];
+    uint32_t I[4], base = 0, par = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        T[j] = fabs_(v[j]);
+        I[j] = (uint32_t)j;
+        if (j < (int)n) {
+            par ^= fbits(v[j]);
+            base |= (fbits(v[j]) >> 31) << j;
+        }
+    }
+    const uint32_t kk = kind == ST_R1 ? 2u : 4u;
+    const uint32_t lim = (n - 1) < kk ? (n - 1) : kk;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        if (t < (int)lim) {
+            float bv = T[t];
+            uint32_t b = (uint32_t)t;
+#pragma unroll
+            for (int j = t + 1; j < 4; ++j) {
+                const bool better = j < (int)n && T[j] < bv;
+                bv = better ? T[j] : bv;
+                b = better ? (uint32_t)j : b;
+            }
+            const uint32_t tv = fbits(T[t]), ti = I[t];
+            uint32_t bi = I[t];
+#pragma unroll
+            for (int j = t + 1; j < 4; ++j) {
+                const uint32_t mj = 0u - (uint32_t)(b == (uint32_t)j);
+                bi = (I[j] & mj) | (bi & ~mj);
+                T[j] = ubits((tv & mj) | (fbits(T[j]) & ~mj));
+                I[j] = (ti & mj) | (I[j] & ~mj);
+            }
+            T[t] = bv;
+            I[t] = bi;
+        }
+    }
+    const uint32_t ib[4] = { 1u << I[0], 1u << I[1], 1u << I[2], 1u << I[3] };
+    if (kind == ST_R1) { // :365-379
+        cv[0] = m;
+        cv[1] = m - T[0];
+        cv[2] = m - T[1];
+        cv[3] = m - T[0] - T[1];
+        pat = base | ((base ^ ib[0]) << 4) | ((base ^ ib[1]) << 8) | ((base ^ ib[0] ^ ib[1]) << 12);
+        return;
+    }
+    // SPC (n = 4): :511-585
+    const bool odd = (par & 0x80000000u) != 0;
+    float mm = m, pinv = 1.0f;
+    if (odd) {
+        pinv = 0.0f;
+        mm -= T[0];
+    }
+    cv[0] = mm;
+    cv[1] = mm - pinv * T[0] - T[1];
+    cv[2] = mm - pinv * T[0] - T[2];
+    cv[3] = mm - pinv * T[0] - T[3];
+    cv[4] = mm - T[1] - T[2];
+    cv[5] = mm - T[1] - T[3];
+    cv[6] = mm - T[2] - T[3];
+    cv[7] = mm - pinv * T[0] - T[1] - T[2] - T[3];
+    pat = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        const uint32_t fm = flip_sel(OP_S_SPC, j, odd ? 1u : 0u);
+        uint32_t fl = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q)
+            fl |= ((fm >> q) & 1u) ? ib[q] : 0u;
+        pat |= ((base ^ fl) & nmask) << (4 * j);
+    }
+}
+
+PCG_DEV void st_r0(St8& st, const float (&v)[4], uint32_t n)
+{
+    float q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        q[j] = 0.0f + minps(j < (int)n && j < 4 ? v[j & 3] : 0.0f, 0.0f);
+    st.m = st.m + ordered8(q);
+}
+
+PCG_DEV void st_branch(const Ctx& c, St8& st, uint32_t kind, const float (&v)[4], uint32_t n, uint32_t boff)
+{
+    const uint32_t k = kind == ST_R1 ? 4u : kind == ST_SPC ? 8u : 2u;
+    const uint32_t lk = kind == ST_R1 ? 2u : kind == ST_SPC ? 3u : 1u;
+    float cv[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
+    uint32_t pat = 0;
+    st_cands(kind, v, n, st.m, cv, pat);
+    float* cval = c.lds + c.ly.cval;
+    if (c.lane < st.P) {
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j)
+            if (j < k)
+                cval[c.lane * k + j] = cv[j];
+    }
+    wsync();
+    const uint32_t C = st.P * k;
+    const uint32_t np = C < c.L ? C : c.L;
+    partial_sort(c, C, np);
+    wsync();
+    const uint32_t* cid = reinterpret_cast<const uint32_t*>(c.lds + c.ly.cid);
+    const uint32_t q = c.lane;
+    const uint32_t id = q < np ? cid[q] : 0u;
+    const float val = q < np ? cval[q] : 0.0f;
+    const int src = (int)(id >> lk);
+    const uint32_t j = id & (k - 1u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        st.x8[i] = shfl(st.x8[i], src);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        st.a4[i] = shfl(st.a4[i], src);
+    st.bits = shfl(st.bits, src);
+    st.root = shfl(st.root, src);
+    pat = shfl(pat, src);
+    st.bits |= ((pat >> (4 * j)) & ((1u << n) - 1u)) << boff;
+    st.m = val;
+    st.P = np;
+    st.branched = true;
+}
+
+PCG_DEV void st_child2(const Ctx& c, St8& st, uint32_t kind, const float (&a2)[4], uint32_t boff)
+{
+    if (kind == ST_R0)
+        st_r0(st, a2, 2);
+    else
+        st_branch(c, st, kind, a2, 2, boff);
+}
+
+PCG_DEV void st_child4(const Ctx& c, St8& st, uint32_t d, uint32_t boff)
+{
+    const uint32_t kind = d & 7u;
+    if (kind == ST_R0) {
+        st_r0(st, st.a4, 4);
+    } else if (kind != ST_RATER) {
+        const float v[4] = { st.a4[0], st.a4[1], st.a4[2], st.a4[3] };
+        st_branch(c, st, kind, v, 4, boff);
+    } else { // ShortRateRNode(4): F, left(2), G, right(2), CombineBitsShort
+        float a2[4] = { polar_f(st.a4[0], st.a4[2]), polar_f(st.a4[1], st.a4[3]), 0.0f, 0.0f };
+        st_child2(c, st, (d >> 3) & 3u, a2, boff);
+        a2[0] = polar_g(st.a4[0], st.a4[2], ((st.bits >> boff) & 1u) << 31);
+        a2[1] = polar_g(st.a4[1], st.a4[3], ((st.bits >> (boff + 1)) & 1u) << 31);
+        st_child2(c, st, (d >> 5) & 3u, a2, boff + 2);
+        st.bits ^= ((st.bits >> (boff + 2)) & 3u) << boff;
+    }
+}
+
+template <typename Src>
+PCG_DEV void st8_run(const Ctx& c, Src src, uint32_t desc, uint32_t o, uint32_t& P, uint32_t& cur)
+{
+    const uint8_t* ptr = ptr_tab(c, cur);
+    float* met = met_tab(c, cur);
+    St8 st;
+    st.P = P;
+    st.branched = false;
+    st.root = c.lane;
+    st.bits = 0;
+    const uint32_t p = c.lane < P ? c.lane : 0u;
+    {
+        const float* x = src.slot(c.top == 3 ? 0u : ptr[p * 16 + 3]);
+        const float4 lo = *reinterpret_cast<const float4*>(x);
+        const float4 hi = *reinterpret_cast<const float4*>(x + 4);
+        st.x8[0] = lo.x; st.x8[1] = lo.y; st.x8[2] = lo.z; st.x8[3] = lo.w;
+        st.x8[4] = hi.x; st.x8[5] = hi.y; st.x8[6] = hi.z; st.x8[7] = hi.w;
+    }
+    st.m = met[p];
+    // F(8) -> left child (4)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        st.a4[i] = polar_f(st.x8[i], st.x8[i + 4]);
+    st_child4(c, st, desc & 0xffu, 0);
+    // G(8) -> right child (4)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        st.a4[i] = polar_g(st.x8[i], st.x8[i + 4], ((st.bits >> i) & 1u) << 31);
+    st_child4(c, st, (desc >> 8) & 0xffu, 4);
+    st.bits ^= (st.bits >> 4) & 0xFu; // CombineBitsShort(4)
+    // write back: metrics, codeword bits [o, o+8), lazy duplicate of the LDS path state
+    const uint32_t sh = o & 31u, wo = o >> 5, msk = 0xFFu << sh;
+    if (!st.branched) {
+        if (c.lane < P) {
+            met[c.lane] = st.m;
+            uint32_t* w = cw_tab(c, cur) + c.lane * c.W + wo;
+            *w = (*w & ~msk) | (st.bits << sh);
+        }
+        return;
+    }
+    const uint32_t nxt = cur ^ 1u, NP = st.P, nw = wo + 1;
+    const uint32_t* cw = cw_tab(c, cur);
+    uint32_t* cw2 = cw_tab(c, nxt);
+    const uint32_t* pt = reinterpret_cast<const uint32_t*>(ptr);
+    uint32_t* pt2 = reinterpret_cast<uint32_t*>(ptr_tab(c, nxt));
+    // survivors' roots and bits through the exchange area (every lane then reads them)
+    uint32_t* xr = reinterpret_cast<uint32_t*>(c.lds + c.ly.xch);
+    if (c.lane < NP) {
+        xr[c.lane] = st.root;
+        xr[32 + c.lane] = st.bits;
+    }
+    wsync();
+    for (uint32_t e = c.lane; e < NP * nw; e += 64) {
+        const uint32_t q = e / nw, w = e - q * nw;
+        uint32_t v = cw[xr[q] * c.W + w];
+        if (w == wo)
+            v = (v & ~msk) | (xr[32 + q] << sh);
+        cw2[q * c.W + w] = v;
+    }
+    for (uint32_t e = c.lane; e < NP * 4; e += 64) {
+        const uint32_t q = e >> 2;
+        pt2[q * 4 + (e & 3)] = pt[xr[q] * 4 + (e & 3)];
+    }
+    if (c.lane < NP)
+        met_tab(c, nxt)[c.lane] = st.m;
+    cur = nxt;
+    P = NP;
+}
+
 template <typename Fn>
 PCG_DEV void with_src(const Ctx& c, uint32_t s, Fn&& fn)
 {
@@ -931,6 +1185,14 @@ __global__ void __launch_bounds__(64) scl_kernel(KernelArgs a)
             case OP_COMB:
                 comb_op(c, s, o, P, cur);
                 break;
+            case OP_S_ST8: {
+                const uint32_t desc = a.ops[++kop];
+                if (c.top == 3)
+                    st8_run(c, ChanStage{ c.y }, desc, o, P, cur);
+                else
+                    st8_run(c, lds_stage(c, 3), desc, o, P, cur);
+                break;
+            }
             case OP_S_R0:
                 if (s <= 3 && s < c.Sl && s != c.top) {
                     small_leaf(c, OP_S_R0, s, P, cur);
@@ -1035,7 +1297,8 @@ int scl_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* lds_
     if (const char* e = getenv("PCG_SCL_LDS_KB"))
         budget = (uint32_t)atoi(e) * 1024 / 4;
     uint32_t Sl = top;
-    while (Sl > 1 && make_layout(N, L, Sl).total > budget)
+    const uint32_t Smin = top < 4 ? top : 4; // ST8 reads stage 3 from LDS
+    while (Sl > Smin && make_layout(N, L, Sl).total > budget)
         --Sl;
     if (const char* e = getenv("PCG_SCL_STAGE_LIMIT")) {
         uint32_t v = (uint32_t)atoi(e);
