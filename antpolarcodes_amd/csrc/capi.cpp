@@ -19,9 +19,9 @@ struct pcg_plan {
     uint32_t* d_crc_m = nullptr;
     uint32_t wave_lds_floats = 0;
     uint32_t lds_stage_limit = 0;
-    uint64_t scratch_floats = 0;  // per codeword
+    uint64_t scratch_floats = 0;  // per scratch unit (codeword or lane-serial wave)
     float* d_scratch = nullptr;   // grown on demand
-    uint64_t scratch_frames = 0;  // capacity in codewords
+    uint64_t scratch_frames = 0;  // capacity in scratch units
     // host-pointer path staging
     float* d_llr = nullptr;
     uint8_t* d_info = nullptr;
@@ -125,7 +125,9 @@ int pcg_plan_create(pcg_plan** out,
     if (L == 1) {
         p->wave_lds_floats = pcg::sc_wave_lds_floats(N);
     } else {
-        rc = pcg::scl_layout(N, L, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats);
+        rc = p->host.scl_kind == 0
+                 ? pcg::sclls_layout(N, L, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats)
+                 : pcg::scl_layout(N, L, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats);
         if (rc != 0) {
             delete p;
             return fail(rc, "list decoding layout unsupported for this N/L");
@@ -154,7 +156,7 @@ int pcg_plan_create(pcg_plan** out,
     const auto& h = p->host;
     hipError_t e;
     if ((e = hipMalloc(&p->d_ops, 4 * std::max<size_t>(1, h.ops.size()))) != hipSuccess ||
-        (e = hipMalloc(&p->d_info_pos, 2 * std::max<size_t>(1, h.info_pos.size()))) != hipSuccess ||
+        (e = hipMalloc(&p->d_info_pos, 2 * (h.info_pos.size() + 2))) != hipSuccess ||
         (e = hipMalloc(&p->d_crc_m, 4 * std::max<size_t>(1, h.crc_m.size()))) != hipSuccess) {
         free_plan_device(p);
         delete p;
@@ -233,13 +235,16 @@ int pcg_decode_f32(pcg_plan* p,
             (void)hipMemset(g_prof, 0, 128 * sizeof(unsigned long long));
         a.prof = g_prof;
     }
+    if (const char* fl = getenv("PCG_FLAGS"))
+        a.flags = (uint32_t)strtoul(fl, nullptr, 0);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc;
     if (h.L == 1) {
         rc = pcg::launch_sc(a, s);
     } else {
         if (p->scratch_floats > 0) {
-            const uint64_t need = pcg::scl_scratch_frames(F);
+            const uint64_t need = h.scl_kind == 0 ? pcg::sclls_units(F, h.L, p->wave_lds_floats)
+                                                  : pcg::scl_scratch_frames(F);
             if (need > p->scratch_frames) {
                 (void)hipFree(p->d_scratch);
                 p->d_scratch = nullptr;
@@ -251,7 +256,7 @@ int pcg_decode_f32(pcg_plan* p,
             }
             a.scratch = p->d_scratch;
         }
-        rc = pcg::launch_scl(a, s);
+        rc = h.scl_kind == 0 ? pcg::launch_sclls(a, s) : pcg::launch_scl(a, s);
     }
     if (rc != 0)
         return fail(rc, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));

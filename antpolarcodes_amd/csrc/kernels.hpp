@@ -23,6 +23,7 @@ struct KernelArgs {
     uint64_t scratch_floats;  // per codeword
     uint32_t lds_stage_limit; // SCL: stages < limit live in LDS
     unsigned long long* prof; // dev-only: per-op-code [cycles, count] (null = off)
+    uint32_t flags;           // dev-only experiment switches (PCG_FLAGS), 0 in production
 };
 
 // LDS floats one SC codeword needs: alpha (N floats, index 0 unused) + packed bits.
@@ -39,4 +40,10 @@ int scl_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* lds_
                uint64_t* scratch_floats);
 // codewords that need scratch at once for a launch of F frames
 uint64_t scl_scratch_frames(uint64_t F);
+// lane-serial SCL kernel (sclls_kernel.hip): per-wave LDS / scratch layout, the
+// number of scratch units (waves) a launch of F frames uses, and the launch
+int sclls_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* lds_stage_limit,
+                 uint64_t* scratch_floats);
+uint64_t sclls_units(uint64_t F, uint32_t L, uint32_t wave_lds_floats);
+int launch_sclls(const KernelArgs& a, hipStream_t stream);
 } // namespace pcg

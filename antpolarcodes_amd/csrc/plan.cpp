@@ -218,7 +218,14 @@ int build_plan(PlanHost& p,
     p.systematic = systematic ? 1 : 0;
     p.crc_kind = crc_kind;
     p.frozen.assign(frozen, frozen + nf);
-    p.scl_st8 = L <= 8 && getenv("PCG_SCL_NO_ST8") == nullptr; // ST8 sorts <= 64 candidates
+    // SCL kernel choice (dev switch PCG_SCL_KERNEL=wave selects the cooperative
+    // one-codeword-per-wave kernel); the lane-serial kernel always runs size-8
+    // subtrees in registers, the cooperative one only for L <= 8 (<= 64 candidates)
+    {
+        const char* k = getenv("PCG_SCL_KERNEL");
+        p.scl_kind = (k && std::string(k) == "wave") ? 1 : 0;
+    }
+    p.scl_st8 = p.scl_kind == 0 || (L <= 8 && getenv("PCG_SCL_NO_ST8") == nullptr);
     try {
         if (L == 1)
             sc_emit(p, p.frozen, N, 0);

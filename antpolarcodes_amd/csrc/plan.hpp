@@ -72,6 +72,7 @@ struct PlanHost {
     uint32_t node_count = 0;
     std::vector<int> node_types;    // pre-order census (op code of each node; 0 = internal)
     bool scl_st8 = true;            // emit lane-serial size-8 subtrees for SCL
+    int scl_kind = 0;               // SCL kernel: 0 lane-serial (sclls_kernel.hip), 1 one codeword per wave
 };
 
 // Returns 0, or a negative pcg.h error code with *err set.

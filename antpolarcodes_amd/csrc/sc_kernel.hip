@@ -390,7 +390,7 @@ __global__ void __launch_bounds__(64 * WAVES) sc_kernel(KernelArgs a)
     const uint32_t top = a.log2N;
 
     for (uint32_t k = 0; k < a.nops; ++k) {
-        const uint32_t w = a.ops[k];
+        const uint32_t w = ld_const(a.ops, k);
         const uint32_t code = op_code(w), s = op_stage(w), o = op_off(w);
         const uint64_t t0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
         if (code >= OP_L_R0) {

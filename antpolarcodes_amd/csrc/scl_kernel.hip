@@ -91,9 +91,30 @@ struct Ctx {
     uint32_t N, L, top, Sl, W;
     Layout ly;
     uint32_t lane;
+    uint32_t flags;         // dev-only experiment switches (PCG_FLAGS)
+    bool regptr;            // L <= 8: slot table in a VGPR (lane t = stage t, 3 bits/path)
+    mutable uint32_t ptrw;  // this lane's stage word of the register slot table
 };
 
+constexpr uint32_t PTR_IDENT = 0xFAC688u; // slot p for path p, 3 bits each (p = 0..7)
+
 PCG_DEV uint8_t* ptr_tab(const Ctx& c, uint32_t cur) { return reinterpret_cast<uint8_t*>(c.lds + c.ly.ptr) + cur * c.L * 16; }
+// Slot of path p at stage s (the reference's lazily shared DataPool block).
+struct PtrView {
+    const uint8_t* base; // LDS table column (regptr == false)
+    uint32_t word;       // uniform packed stage word (regptr == true)
+    bool reg;
+    PCG_DEV uint32_t slot(uint32_t p) const { return reg ? (word >> (3 * p)) & 7u : base[p * 16]; }
+};
+PCG_DEV PtrView ptr_view(const Ctx& c, uint32_t s, uint32_t cur)
+{
+    PtrView v;
+    v.reg = c.regptr;
+    v.base = ptr_tab(c, cur) + s;
+    v.word = c.regptr ? (uint32_t)__builtin_amdgcn_readlane((int)c.ptrw, (int)s) : 0u;
+    return v;
+}
+
 PCG_DEV uint32_t* cw_tab(const Ctx& c, uint32_t cur) { return reinterpret_cast<uint32_t*>(c.lds + c.ly.cw0) + cur * c.L * c.W; }
 PCG_DEV float* met_tab(const Ctx& c, uint32_t cur) { return c.lds + c.ly.met + cur * c.L; }
 
@@ -127,7 +148,7 @@ template <int OPC, typename Src, typename Dst>
 PCG_DEV void fg_op(const Ctx& c, Src src, Dst dst, uint32_t s, uint32_t o, uint32_t P, uint32_t cur)
 {
     const uint32_t h = 1u << (s - 1), lh = s - 1;
-    const uint8_t* ptr = ptr_tab(c, cur);
+    const PtrView pv = ptr_view(c, s, cur);
     const uint32_t* cw = cw_tab(c, cur);
     const uint32_t tot = P << lh;
     if (h >= 4) {
@@ -139,7 +160,7 @@ PCG_DEV void fg_op(const Ctx& c, Src src, Dst dst, uint32_t s, uint32_t o, uint3
                 const uint32_t e = e0 + 256 * u;
                 if (e < tot) {
                     const uint32_t p = e >> lh, i = e & (h - 1);
-                    const auto* in = src.slot(s == c.top ? 0u : ptr[p * 16 + s]);
+                    const auto* in = src.slot(s == c.top ? 0u : pv.slot(p));
                     xa[u] = *reinterpret_cast<const float4*>(in + i);
                     xb[u] = *reinterpret_cast<const float4*>(in + i + h);
                     if (OPC == OP_G)
@@ -170,7 +191,7 @@ PCG_DEV void fg_op(const Ctx& c, Src src, Dst dst, uint32_t s, uint32_t o, uint3
     } else {
         for (uint32_t e = c.lane; e < tot; e += 64) {
             const uint32_t p = e >> lh, i = e & (h - 1);
-            const auto* in = src.slot(s == c.top ? 0u : ptr[p * 16 + s]);
+            const auto* in = src.slot(s == c.top ? 0u : pv.slot(p));
             float r;
             if (OPC == OP_F)
                 r = polar_f(in[i], in[i + h]);
@@ -185,7 +206,9 @@ template <int OPC>
 PCG_DEV void fg_dispatch(const Ctx& c, uint32_t s, uint32_t o, uint32_t P, uint32_t cur)
 {
     const uint32_t d = s - 1;
-    if (s == c.top) {
+    if (c.flags & 2u) {
+        // timing experiment only (PCG_FLAGS): skip the arithmetic
+    } else if (s == c.top) {
         if (d >= c.Sl)
             fg_op<OPC>(c, ChanStage{ c.y }, gl_stage(c, d), s, o, P, cur);
         else
@@ -200,9 +223,13 @@ PCG_DEV void fg_dispatch(const Ctx& c, uint32_t s, uint32_t o, uint32_t P, uint3
     }
     wsync();
     // every path now owns slot p of stage d
-    uint8_t* ptr = ptr_tab(c, cur);
-    for (uint32_t p = c.lane; p < P; p += 64)
-        ptr[p * 16 + d] = (uint8_t)p;
+    if (c.regptr) {
+        c.ptrw = c.lane == d ? PTR_IDENT : c.ptrw;
+    } else {
+        uint8_t* ptr = ptr_tab(c, cur);
+        for (uint32_t p = c.lane; p < P; p += 64)
+            ptr[p * 16 + d] = (uint8_t)p;
+    }
 }
 
 // COMB at stage s: cw[p][o+i] ^= cw[p][o+h+i], i < h
@@ -259,13 +286,13 @@ template <typename Src>
 PCG_DEV void leaf_r0(const Ctx& c, Src src, uint32_t s, uint32_t o, uint32_t P, uint32_t cur)
 {
     const uint32_t n = 1u << s;
-    const uint8_t* ptr = ptr_tab(c, cur);
+    const PtrView pv = ptr_view(c, s, cur);
     float* met = met_tab(c, cur);
     for (uint32_t p0 = 0; p0 < P; p0 += 8) {
         const uint32_t p = p0 + (c.lane >> 3), j = c.lane & 7;
         float acc = 0.0f;
         if (p < P) {
-            const float* in = src.slot(s == c.top ? 0u : ptr[p * 16 + s]);
+            const float* in = src.slot(s == c.top ? 0u : pv.slot(p));
             if (n < 8) {
                 acc = acc + minps(j < n ? in[j] : 0.0f, 0.0f);
             } else {
@@ -301,14 +328,14 @@ template <typename Src>
 PCG_DEV void cand_rep(const Ctx& c, Src src, uint32_t s, uint32_t P, uint32_t cur)
 {
     const uint32_t n = 1u << s;
-    const uint8_t* ptr = ptr_tab(c, cur);
+    const PtrView pv = ptr_view(c, s, cur);
     const float* met = met_tab(c, cur);
     float* cval = c.lds + c.ly.cval;
     for (uint32_t p0 = 0; p0 < P; p0 += 8) {
         const uint32_t p = p0 + (c.lane >> 3), j = c.lane & 7;
         float l = 0.0f;
         if (p < P) {
-            const float* in = src.slot(s == c.top ? 0u : ptr[p * 16 + s]);
+            const float* in = src.slot(s == c.top ? 0u : pv.slot(p));
             l = j < n ? in[j] : 0.0f;
         }
         const float z = 0.0f + minps(l, 0.0f);
@@ -343,7 +370,7 @@ PCG_DEV void weak_search(const Ctx& c, Src src, uint32_t s, uint32_t P, uint32_t
     const uint32_t lg = __builtin_ctz(g);
     const uint32_t gpp = 64 >> lg; // paths per pass
     const uint32_t gl = c.lane & (g - 1);
-    const uint8_t* ptr = ptr_tab(c, cur);
+    const PtrView pv = ptr_view(c, s, cur);
     float* wk = c.lds + c.ly.wk;
     uint32_t* wi = reinterpret_cast<uint32_t*>(c.lds + c.ly.wi);
     uint32_t* wpar = reinterpret_cast<uint32_t*>(c.lds + c.ly.wpar);
@@ -351,7 +378,7 @@ PCG_DEV void weak_search(const Ctx& c, Src src, uint32_t s, uint32_t P, uint32_t
     for (uint32_t p0 = 0; p0 < P; p0 += gpp) {
         const uint32_t p = p0 + (c.lane >> lg);
         const bool act = p < P;
-        const float* in = src.slot(s == c.top ? 0u : ptr[(act ? p : 0) * 16 + s]);
+        const float* in = src.slot(s == c.top ? 0u : pv.slot(act ? p : 0));
         uint32_t par = 0;
         if (act)
             for (uint32_t i = gl; i < n; i += g)
@@ -473,11 +500,11 @@ PCG_DEV float ordered8(const float (&a)[8])
 PCG_DEV void small_leaf(const Ctx& c, uint32_t code, uint32_t s, uint32_t P, uint32_t cur)
 {
     const uint32_t n = 1u << s, p = c.lane;
+    const PtrView pv = ptr_view(c, s, cur);
     if (p >= P)
         return;
-    const uint8_t* ptr = ptr_tab(c, cur);
     float* met = met_tab(c, cur);
-    const float* x = lds_stage(c, s).slot(ptr[p * 16 + s]);
+    const float* x = lds_stage(c, s).slot(pv.slot(p));
     float v[8];
     load8(x, n, v);
     const float m = met[p];
@@ -804,9 +831,17 @@ PCG_DEV void branch_commit(const Ctx& c, Src src, uint32_t code, uint32_t s, uin
         const uint32_t srcp = cid[q] / k;
         cw2[q * c.W + w] = cw[srcp * c.W + w];
     }
-    for (uint32_t e = c.lane; e < np * 4; e += 64) {
-        const uint32_t q = e >> 2, w = e & 3;
-        reinterpret_cast<uint32_t*>(ptr2)[q * 4 + w] = reinterpret_cast<const uint32_t*>(ptr)[(cid[q] / k) * 4 + w];
+    const PtrView pv = ptr_view(c, s, cur); // the leaf's own stage, read before the table changes
+    if (c.regptr) {
+        uint32_t nw2 = 0;
+        for (uint32_t q = 0; q < np; ++q)
+            nw2 |= ((c.ptrw >> (3 * (cid[q] / k))) & 7u) << (3 * q);
+        c.ptrw = nw2;
+    } else {
+        for (uint32_t e = c.lane; e < np * 4; e += 64) {
+            const uint32_t q = e >> 2, w = e & 3;
+            reinterpret_cast<uint32_t*>(ptr2)[q * 4 + w] = reinterpret_cast<const uint32_t*>(ptr)[(cid[q] / k) * 4 + w];
+        }
     }
     for (uint32_t q = c.lane; q < np; q += 64)
         met2[q] = cval[q];
@@ -829,7 +864,7 @@ PCG_DEV void branch_commit(const Ctx& c, Src src, uint32_t code, uint32_t s, uin
                     wq[t] = wi[srcp * 4 + t];
             }
         }
-        const float* in = src.slot(s == c.top ? 0u : ptr[(act ? srcp : 0) * 16 + s]);
+        const float* in = src.slot(s == c.top ? 0u : pv.slot(act ? srcp : 0));
         for (uint32_t b = 0; b < n; b += g) {
             const uint32_t i = b + gl;
             uint32_t bit = 0;
@@ -1073,6 +1108,7 @@ template <typename Src>
 PCG_DEV void st8_run(const Ctx& c, Src src, uint32_t desc, uint32_t o, uint32_t& P, uint32_t& cur)
 {
     const uint8_t* ptr = ptr_tab(c, cur);
+    const PtrView pv = ptr_view(c, 3, cur);
     float* met = met_tab(c, cur);
     St8 st;
     st.P = P;
@@ -1081,7 +1117,7 @@ PCG_DEV void st8_run(const Ctx& c, Src src, uint32_t desc, uint32_t o, uint32_t&
     st.bits = 0;
     const uint32_t p = c.lane < P ? c.lane : 0u;
     {
-        const float* x = src.slot(c.top == 3 ? 0u : ptr[p * 16 + 3]);
+        const float* x = src.slot(c.top == 3 ? 0u : pv.slot(p));
         const float4 lo = *reinterpret_cast<const float4*>(x);
         const float4 hi = *reinterpret_cast<const float4*>(x + 4);
         st.x8[0] = lo.x; st.x8[1] = lo.y; st.x8[2] = lo.z; st.x8[3] = lo.w;
@@ -1128,9 +1164,16 @@ PCG_DEV void st8_run(const Ctx& c, Src src, uint32_t desc, uint32_t o, uint32_t&
             v = (v & ~msk) | (xr[32 + q] << sh);
         cw2[q * c.W + w] = v;
     }
-    for (uint32_t e = c.lane; e < NP * 4; e += 64) {
-        const uint32_t q = e >> 2;
-        pt2[q * 4 + (e & 3)] = pt[xr[q] * 4 + (e & 3)];
+    if (c.regptr) {
+        uint32_t nw2 = 0;
+        for (uint32_t q = 0; q < NP; ++q)
+            nw2 |= ((c.ptrw >> (3 * xr[q])) & 7u) << (3 * q);
+        c.ptrw = nw2;
+    } else {
+        for (uint32_t e = c.lane; e < NP * 4; e += 64) {
+            const uint32_t q = e >> 2;
+            pt2[q * 4 + (e & 3)] = pt[xr[q] * 4 + (e & 3)];
+        }
     }
     if (c.lane < NP)
         met_tab(c, nxt)[c.lane] = st.m;
@@ -1154,15 +1197,33 @@ PCG_DEV void with_src(const Ctx& c, uint32_t s, Fn&& fn)
 __global__ void __launch_bounds__(64) scl_kernel(KernelArgs a)
 {
     extern __shared__ float smem[];
+#ifdef PCG_SPECIAL
+    unsigned long long* const prof = nullptr;
+#else
+    unsigned long long* const prof = a.prof;
+#endif
     Ctx c;
     c.lds = smem;
+#ifdef PCG_SPECIAL
+    c.N = 1024; c.L = 8; c.top = 10; c.Sl = 7; c.W = 32;
+    c.ly = make_layout(1024, 8, 7);
+#else
     c.N = a.N;
     c.L = a.L;
     c.top = a.log2N;
     c.Sl = a.lds_stage_limit;
     c.W = a.N >= 32 ? a.N / 32 : 1;
     c.ly = make_layout(a.N, a.L, a.lds_stage_limit);
+#endif
     c.lane = threadIdx.x;
+#ifdef PCG_SPECIAL
+    c.regptr = true;
+    c.flags = 0;
+#else
+    c.regptr = a.L <= 8 && !(a.flags & 1u);
+    c.flags = a.flags;
+#endif
+    c.ptrw = PTR_IDENT;
     c.gs = a.scratch ? a.scratch + (uint64_t)blockIdx.x * a.scratch_floats : nullptr;
 
     for (uint64_t frame = blockIdx.x; frame < a.F; frame += gridDim.x) {
@@ -1172,9 +1233,10 @@ __global__ void __launch_bounds__(64) scl_kernel(KernelArgs a)
             met_tab(c, 0)[0] = 0.0f; // a freshly constructed decoder
         wsync();
         for (uint32_t kop = 0; kop < a.nops; ++kop) {
-            const uint32_t w = a.ops[kop];
+            // readfirstlane keeps the schedule walk wave-uniform, so ops are s_load'ed
+            const uint32_t w = ld_const(a.ops, kop);
             const uint32_t code = op_code(w), s = op_stage(w), o = op_off(w);
-            const uint64_t t0 = a.prof ? __builtin_amdgcn_s_memtime() : 0;
+            const uint64_t t0 = prof ? __builtin_amdgcn_s_memtime() : 0;
             switch (code) {
             case OP_F:
                 fg_dispatch<OP_F>(c, s, o, P, cur);
@@ -1183,10 +1245,13 @@ __global__ void __launch_bounds__(64) scl_kernel(KernelArgs a)
                 fg_dispatch<OP_G>(c, s, o, P, cur);
                 break;
             case OP_COMB:
-                comb_op(c, s, o, P, cur);
+                if (!(c.flags & 32u))
+                    comb_op(c, s, o, P, cur);
                 break;
             case OP_S_ST8: {
-                const uint32_t desc = a.ops[++kop];
+                const uint32_t desc = ld_const(a.ops, ++kop);
+                if (c.flags & 8u)
+                    break;
                 if (c.top == 3)
                     st8_run(c, ChanStage{ c.y }, desc, o, P, cur);
                 else
@@ -1194,6 +1259,8 @@ __global__ void __launch_bounds__(64) scl_kernel(KernelArgs a)
                 break;
             }
             case OP_S_R0:
+                if (c.flags & 128u)
+                    break;
                 if (s <= 3 && s < c.Sl && s != c.top) {
                     small_leaf(c, OP_S_R0, s, P, cur);
                     wsync();
@@ -1203,12 +1270,14 @@ __global__ void __launch_bounds__(64) scl_kernel(KernelArgs a)
                 }
                 break;
             default: { // branching leaves
+                if (c.flags & 16u)
+                    break;
                 const uint32_t k = code == OP_S_R1 ? 4 : code == OP_S_SPC ? 8 : 2;
                 auto stamp = [&](uint32_t ph, uint64_t& tp) {
-                    if (a.prof) {
+                    if (prof) {
                         const uint64_t tn = __builtin_amdgcn_s_memtime();
                         if (c.lane == 0)
-                            atomicAdd(&a.prof[2 * ph], (unsigned long long)(tn - tp));
+                            atomicAdd(&prof[2 * ph], (unsigned long long)(tn - tp));
                         tp = tn;
                     }
                 };
@@ -1227,7 +1296,12 @@ __global__ void __launch_bounds__(64) scl_kernel(KernelArgs a)
                 stamp(49, tp);
                 const uint32_t C = P * k;
                 const uint32_t np = C < c.L ? C : c.L;
-                partial_sort(c, C, np);
+                if (c.flags & 4u) {
+                    if (c.lane < np)
+                        reinterpret_cast<uint32_t*>(c.lds + c.ly.cid)[c.lane] = c.lane;
+                } else {
+                    partial_sort(c, C, np);
+                }
                 wsync();
                 stamp(50, tp);
                 with_src(c, s, [&](auto src) { branch_commit(c, src, code, s, o, P, np, k, cur); });
@@ -1239,11 +1313,11 @@ __global__ void __launch_bounds__(64) scl_kernel(KernelArgs a)
             }
             }
             wsync();
-            if (a.prof) {
+            if (prof) {
                 const uint64_t t1 = __builtin_amdgcn_s_memtime();
                 if (c.lane == 0) {
-                    atomicAdd(&a.prof[2 * code], (unsigned long long)(t1 - t0));
-                    atomicAdd(&a.prof[2 * code + 1], 1ull);
+                    atomicAdd(&prof[2 * code], (unsigned long long)(t1 - t0));
+                    atomicAdd(&prof[2 * code + 1], 1ull);
                 }
             }
         }
@@ -1265,7 +1339,7 @@ __global__ void __launch_bounds__(64) scl_kernel(KernelArgs a)
             }
         }
         uint32_t chosen = 0, found = 0;
-        for (uint32_t p = 0; p < P; ++p) {
+        for (uint32_t p = 0; p < P && !(c.flags & 64u); ++p) {
             uint32_t syn;
             write_bits_from_info(c, a, cwc + p * c.W, frame, false, &syn);
             if (syn == 0) {
@@ -1322,7 +1396,10 @@ uint64_t scl_scratch_frames(uint64_t F)
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess)
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        g_resident_cap = (uint64_t)cus * 16; // grid cap (grid-stride over frames)
+        uint64_t wpc = 16;
+        if (const char* e = getenv("PCG_SCL_WPC"))
+            wpc = (uint64_t)atoi(e);
+        g_resident_cap = (uint64_t)cus * wpc; // grid cap (grid-stride over frames)
     }
     return F < g_resident_cap ? F : g_resident_cap;
 }

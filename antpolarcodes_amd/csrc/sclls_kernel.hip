@@ -1,0 +1,1048 @@
+// sclls_kernel.hip -- lane-serial batched CRC-aided SCL polar decoding on CDNA4 (gfx950).
+//
+// Lane = one path of one codeword.  A wave decodes G = 64 / LP codewords at once
+// (LP = list size rounded up to a power of two), lanes g*LP .. g*LP+LP-1 holding the
+// paths of codeword g.  Every codeword shares the plan's schedule and the path count
+// P after each leaf only depends on the schedule, so the wave walks the schedule
+// uniformly and each lane runs the reference's per-path loops literally (the AVX
+// decoder's own order of operations, scl_avx_float.cpp), serially over the node's
+// LLRs.  Compared with the cooperative one-codeword-per-wave kernel this removes the
+// per-op address arithmetic, reductions and LDS round trips that dominated there:
+// elementwise F/G become float4 streams with plenty of independent loads per lane.
+//
+// State of path p (lane l = g*LP + p):
+//   * metric m (register);
+//   * LLR stage buffers alpha[s] for stages 3 <= s < top, element chunk c (4 floats)
+//     of lane l at ((c * 64) + l) * 4 -- LDS for s < Sl, a per-wave global scratch
+//     slab (L2/MALL resident) for s >= Sl; stages < 3 only exist inside size-8
+//     subtrees, which run in registers (OP_S_ST8);
+//   * a slot table ptr (5 bits per stage): alpha[s] of path p lives in lane
+//     g*LP + slot_s.  An F/G at stage s rewrites every path's alpha[s-1] (all old
+//     ones are dead then) in its own lane; a branching leaf copies the table row of
+//     the path each survivor descends from -- the reference's lazy DataPool copy
+//     (scl_avx_float.cpp:21-171) without moving any LLRs;
+//   * the packed codeword bits of the path, one LDS word column per lane.
+// Path selection (simplePartialSortDescending, arrayfuncs.h:161-183) is a merge of
+// the LP lanes' locally sorted candidate lists; exact ties (the only case where the
+// reference's swap order is observable) switch the wave to a literal simulation.
+#include "kernels.hpp"
+#include "plan.hpp"
+#include "wave.hpp"
+
+#include <stdlib.h>
+
+namespace pcg {
+
+namespace {
+
+constexpr uint32_t LS_MINS = 3; // lowest memory stage: size-8 nodes
+
+// ---- layout --------------------------------------------------------------------------
+struct LsLayout {
+    uint32_t alpha; // 64 * (2^Sl - 8) floats (stages [3, Sl))
+    uint32_t bits;  // 64 * W words
+    uint32_t cval;  // 64 * 8 floats: tie fallback candidate list
+    uint32_t cid;   // 64 * 8 words
+    uint32_t total;
+};
+
+__host__ __device__ inline LsLayout ls_layout(uint32_t N, uint32_t Sl)
+{
+    LsLayout y;
+    uint32_t o = 0;
+    y.alpha = o;
+    o += Sl > LS_MINS ? 64u * ((1u << Sl) - 8u) : 0u;
+    y.bits = o;
+    o += 64u * (N >= 32 ? N / 32 : 1u);
+    y.cval = o;
+    o += 512;
+    y.cid = o;
+    o += 512;
+    y.total = o;
+    return y;
+}
+
+// ---- per-wave context ----------------------------------------------------------------
+template <int LP>
+struct Ls {
+    float* lds;
+    float* gs;        // this wave's global scratch slab
+    const float* y;   // this lane's codeword channel LLRs
+    uint32_t N, L, top, Sl;
+    LsLayout ly;
+    uint32_t lane, p, gb; // lane, path index in the group, group base lane
+    uint64_t ptr;         // slot of stage s at bits 5(s-3)
+    float m;              // path metric
+    PCG_DEV uint32_t src_lane(uint32_t s) const { return gb | (uint32_t)((ptr >> (5u * (s - LS_MINS))) & 31u); }
+    PCG_DEV void own(uint32_t s) { // alpha[s] of this path is now in its own lane
+        const uint32_t sh = 5u * (s - LS_MINS);
+        ptr = (ptr & ~(31ull << sh)) | ((uint64_t)p << sh);
+    }
+    PCG_DEV uint32_t* row() const { return reinterpret_cast<uint32_t*>(lds + ly.bits) + lane; } // word w at [w*64]
+    PCG_DEV uint32_t* row_of(uint32_t l) const { return reinterpret_cast<uint32_t*>(lds + ly.bits) + l; }
+};
+
+// Stage storages.  ld(c, l): float4 chunk c of lane l's buffer; st(c, v): own lane.
+struct LdsSt {
+    float* b;
+    uint32_t lane;
+    PCG_DEV float4 ld(uint32_t c, uint32_t l) const { return *reinterpret_cast<const float4*>(b + ((c << 6) + l) * 4u); }
+    PCG_DEV void st(uint32_t c, const float4& v) const { *reinterpret_cast<float4*>(b + ((c << 6) + lane) * 4u) = v; }
+};
+struct GlSt {
+    float* b;
+    uint32_t lane;
+    PCG_DEV float4 ld(uint32_t c, uint32_t l) const { return *reinterpret_cast<const float4*>(b + ((uint64_t)((c << 6) + l)) * 4u); }
+    PCG_DEV void st(uint32_t c, const float4& v) const { *reinterpret_cast<float4*>(b + ((uint64_t)((c << 6) + lane)) * 4u) = v; }
+};
+struct ChSt { // the channel LLRs of the lane's own codeword (stage top)
+    const float* y;
+    PCG_DEV float4 ld(uint32_t c, uint32_t) const { return reinterpret_cast<const float4*>(y)[c]; }
+};
+
+template <int LP>
+PCG_DEV LdsSt lds_st(const Ls<LP>& c, uint32_t s)
+{
+    return LdsSt{ c.lds + c.ly.alpha + 64u * ((1u << s) - 8u), c.lane };
+}
+template <int LP>
+PCG_DEV GlSt gl_st(const Ls<LP>& c, uint32_t s)
+{
+    return GlSt{ c.gs + 64ull * ((1ull << s) - (1ull << c.Sl)), c.lane };
+}
+
+// Run fn with the storage of stage s (wave-uniform choice).
+template <int LP, typename Fn>
+PCG_DEV void with_stage(const Ls<LP>& c, uint32_t s, Fn&& fn)
+{
+    if (s == c.top)
+        fn(ChSt{ c.y });
+    else if (s >= c.Sl)
+        fn(gl_st(c, s));
+    else
+        fn(lds_st(c, s));
+}
+
+// ---- F / G ---------------------------------------------------------------------------
+// alpha[s-1] of every active path from alpha[s] of its slot (avx_float.h:101-164),
+// h = 2^(s-1) >= 8 elements = hq float4 chunks; 4 chunks in flight per lane.
+template <int OPC, int LP, typename Src, typename Dst>
+PCG_DEV void ls_fg(const Ls<LP>& c, Src src, Dst dst, uint32_t s, uint32_t o, bool act)
+{
+    const uint32_t hq = 1u << (s - 3);
+    const uint32_t sl = s == c.top ? 0u : c.src_lane(s);
+    const uint32_t* row = c.row();
+    if (!act)
+        return;
+    for (uint32_t c0 = 0; c0 < hq; c0 += 4) {
+        float4 xa[4], xb[4];
+        uint32_t wb[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) {
+            if (c0 + u < hq) {
+                xa[u] = src.ld(c0 + u, sl);
+                xb[u] = src.ld(c0 + u + hq, sl);
+                if (OPC == OP_G) {
+                    const uint32_t i = o + 4u * (c0 + u);
+                    wb[u] = row[(i >> 5) << 6] >> (i & 31u);
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u) {
+            if (c0 + u < hq) {
+                float4 r;
+                if (OPC == OP_F) {
+                    r.x = polar_f(xa[u].x, xb[u].x);
+                    r.y = polar_f(xa[u].y, xb[u].y);
+                    r.z = polar_f(xa[u].z, xb[u].z);
+                    r.w = polar_f(xa[u].w, xb[u].w);
+                } else {
+                    r.x = polar_g(xa[u].x, xb[u].x, (wb[u] & 1u) << 31);
+                    r.y = polar_g(xa[u].y, xb[u].y, ((wb[u] >> 1) & 1u) << 31);
+                    r.z = polar_g(xa[u].z, xb[u].z, ((wb[u] >> 2) & 1u) << 31);
+                    r.w = polar_g(xa[u].w, xb[u].w, ((wb[u] >> 3) & 1u) << 31);
+                }
+                dst.st(c0 + u, r);
+            }
+        }
+    }
+}
+
+template <int OPC, int LP>
+PCG_DEV void ls_fg_op(Ls<LP>& c, uint32_t s, uint32_t o, bool act)
+{
+    const uint32_t d = s - 1;
+    if (d >= c.Sl)
+        with_stage(c, s, [&](auto src) { ls_fg<OPC>(c, src, gl_st(c, d), s, o, act); });
+    else
+        with_stage(c, s, [&](auto src) { ls_fg<OPC>(c, src, lds_st(c, d), s, o, act); });
+    c.own(d);
+}
+
+// Combine (avx_float.h:188-197 on packed bits): bit[o+i] ^= bit[o+h+i], i < h.
+template <int LP>
+PCG_DEV void ls_comb(const Ls<LP>& c, uint32_t s, uint32_t o, bool act)
+{
+    const uint32_t h = 1u << (s - 1);
+    uint32_t* row = c.row();
+    if (!act)
+        return;
+    if (h >= 32) {
+        const uint32_t wl = o >> 5, wr = (o + h) >> 5, nw = h >> 5;
+        for (uint32_t w = 0; w < nw; ++w)
+            row[(wl + w) << 6] ^= row[(wr + w) << 6];
+    } else {
+        const uint32_t sh = o & 31u, msk = ((1u << h) - 1u) << sh;
+        uint32_t* w = row + ((o >> 5) << 6);
+        *w ^= (*w >> h) & msk;
+    }
+}
+
+// Clear bits [o, o+n) of the lane's row (Rate-0: all-zero estimate).
+template <int LP>
+PCG_DEV void ls_clear(const Ls<LP>& c, uint32_t n, uint32_t o)
+{
+    uint32_t* row = c.row();
+    if (n >= 32) {
+        for (uint32_t w = o >> 5; w < (o + n) >> 5; ++w)
+            row[w << 6] = 0u;
+    } else {
+        row[(o >> 5) << 6] &= ~(((1u << n) - 1u) << (o & 31u));
+    }
+}
+
+// ---- Rate-0 leaf, n >= 8 (scl_avx_float.cpp:316-337) ----------------------------------
+// metric += reduce_add_ps(sum over 8-float vectors of min(llr, +0)): lane j of the AVX
+// accumulator takes elements j, j+8, ... from +0, then ((((((a0+a1)+a2)+a3)+a4)+a5)+a6)+a7.
+template <int LP, typename Src>
+PCG_DEV void ls_r0(Ls<LP>& c, Src src, uint32_t s, uint32_t o, bool act)
+{
+    const uint32_t nq = 1u << (s - 2);
+    const uint32_t sl = s == c.top ? 0u : c.src_lane(s);
+    if (!act)
+        return;
+    float acc[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
+    for (uint32_t q = 0; q < nq; q += 2) {
+        const float4 a = src.ld(q, sl), b = src.ld(q + 1, sl);
+        acc[0] = acc[0] + minps(a.x, 0.0f);
+        acc[1] = acc[1] + minps(a.y, 0.0f);
+        acc[2] = acc[2] + minps(a.z, 0.0f);
+        acc[3] = acc[3] + minps(a.w, 0.0f);
+        acc[4] = acc[4] + minps(b.x, 0.0f);
+        acc[5] = acc[5] + minps(b.y, 0.0f);
+        acc[6] = acc[6] + minps(b.z, 0.0f);
+        acc[7] = acc[7] + minps(b.w, 0.0f);
+    }
+    float r = acc[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j)
+        r = r + acc[j];
+    c.m = c.m + r;
+    ls_clear(c, 1u << s, o);
+}
+
+// ---- weak positions: findWeakLlrs(idx, |llr|, n, kk) (arrayfuncs.h:209-231) ------------
+// Exact selection passes with the reference's swaps: pass t takes the first minimum
+// of positions >= t; the element it displaces is tracked in a <= 4 entry overlay.
+// Results T[t] (value) and I[t] (original index) for t < kk, and the XOR of the n
+// sign bits.  n >= 16 (size-8 leaves use the register version).
+template <int LP, typename Src>
+PCG_DEV void ls_weak(const Ls<LP>& c, Src src, uint32_t sl, uint32_t n, uint32_t kk, float (&T)[4],
+                     uint32_t (&I)[4], uint32_t& par)
+{
+    const uint32_t nq = n >> 2;
+    par = 0;
+    uint32_t ovp[4] = { ~0u, ~0u, ~0u, ~0u }, ovi[4] = { 0, 0, 0, 0 };
+    float ovv[4] = { 0, 0, 0, 0 };
+#pragma unroll
+    for (uint32_t t = 0; t < 4; ++t) {
+        T[t] = 0.0f;
+        I[t] = t;
+        if (t >= kk)
+            continue;
+        // scan raw positions > t that are not in the overlay; the overlay and
+        // position t itself are merged afterwards by (value, position)
+        float bv = __builtin_inff();
+        uint32_t bi = ~0u;
+        for (uint32_t q = 0; q < nq; ++q) {
+            const float4 x = src.ld(q, sl);
+            if (t == 0)
+                par ^= fbits(x.x) ^ fbits(x.y) ^ fbits(x.z) ^ fbits(x.w);
+            const float xv[4] = { x.x, x.y, x.z, x.w };
+#pragma unroll
+            for (uint32_t e = 0; e < 4; ++e) {
+                const uint32_t i = 4u * q + e;
+                bool ok = i > t;
+#pragma unroll
+                for (uint32_t r = 0; r < 4; ++r)
+                    if (r < t)
+                        ok = ok && i != ovp[r];
+                const float v = fabs_(xv[e]);
+                if (ok && (bi == ~0u || v < bv)) {
+                    bv = v;
+                    bi = i;
+                }
+            }
+        }
+        // the element currently at position t
+        float vt;
+        {
+            const float4 x = src.ld(t >> 2, sl);
+            const uint32_t e = t & 3u;
+            vt = fabs_(e == 0 ? x.x : e == 1 ? x.y : e == 2 ? x.z : x.w);
+        }
+        uint32_t it = t;
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r)
+            if (r < t && ovp[r] == t) {
+                vt = ovv[r];
+                it = ovi[r];
+            }
+        // overlay entries at positions > t compete by (value, position)
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r) {
+            if (r < t && ovp[r] != ~0u && ovp[r] > t &&
+                (bi == ~0u || ovv[r] < bv || (ovv[r] == bv && ovp[r] < bi))) {
+                bv = ovv[r];
+                bi = ovp[r];
+            }
+        }
+        // position t itself wins ties (it comes first)
+        uint32_t bo;
+        if (bi == ~0u || !(bv < vt)) {
+            bv = vt;
+            bi = t;
+            bo = it;
+        } else {
+            bo = bi;
+#pragma unroll
+            for (uint32_t r = 0; r < 4; ++r)
+                if (r < t && ovp[r] == bi)
+                    bo = ovi[r];
+        }
+        T[t] = bv;
+        I[t] = bo;
+        if (bi != t) { // the element at position t moves to position bi
+            bool placed = false;
+#pragma unroll
+            for (uint32_t r = 0; r < 4; ++r)
+                if (r < t && ovp[r] == bi) {
+                    ovv[r] = vt;
+                    ovi[r] = it;
+                    placed = true;
+                }
+            if (!placed) {
+                ovp[t] = bi;
+                ovv[t] = vt;
+                ovi[t] = it;
+            }
+        }
+    }
+}
+
+// Register version for n == 8 (and the same selection passes as ls_weak).
+PCG_DEV void weak8(const float (&v)[8], uint32_t kk, float (&T4)[4], uint32_t (&I4)[4], uint32_t& par)
+{
+    float T[8];
+    uint32_t I[8];
+    par = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        T[j] = fabs_(v[j]);
+        I[j] = (uint32_t)j;
+        par ^= fbits(v[j]);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        if (t < (int)kk) {
+            float bv = T[t];
+            uint32_t b = (uint32_t)t;
+#pragma unroll
+            for (int j = t + 1; j < 8; ++j) {
+                const bool better = T[j] < bv;
+                bv = better ? T[j] : bv;
+                b = better ? (uint32_t)j : b;
+            }
+            const uint32_t tv = fbits(T[t]), ti = I[t];
+            uint32_t bi = I[t];
+#pragma unroll
+            for (int j = t + 1; j < 8; ++j) {
+                const uint32_t mj = 0u - (uint32_t)(b == (uint32_t)j);
+                bi = (I[j] & mj) | (bi & ~mj);
+                T[j] = ubits((tv & mj) | (fbits(T[j]) & ~mj));
+                I[j] = (ti & mj) | (I[j] & ~mj);
+            }
+            T[t] = bv;
+            I[t] = bi;
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        T4[t] = T[t];
+        I4[t] = I[t];
+    }
+}
+
+// Candidate metrics of Rate-1 (:365-379, 4 candidates) and SPC (:511-585, 8).
+PCG_DEV void r1_spc_cands(uint32_t code, float m, const float (&T)[4], uint32_t par, float (&cv)[8])
+{
+    if (code == OP_S_R1) {
+        cv[0] = m;
+        cv[1] = m - T[0];
+        cv[2] = m - T[1];
+        cv[3] = m - T[0] - T[1];
+        cv[4] = cv[5] = cv[6] = cv[7] = 0.0f;
+        return;
+    }
+    float mm = m, pinv = 1.0f;
+    if (par & 0x80000000u) { // odd parity: the reference charges T0 up front
+        pinv = 0.0f;
+        mm -= T[0];
+    }
+    cv[0] = mm;
+    cv[1] = mm - pinv * T[0] - T[1];
+    cv[2] = mm - pinv * T[0] - T[2];
+    cv[3] = mm - pinv * T[0] - T[3];
+    cv[4] = mm - T[1] - T[2];
+    cv[5] = mm - T[1] - T[3];
+    cv[6] = mm - T[2] - T[3];
+    cv[7] = mm - pinv * T[0] - T[1] - T[2] - T[3];
+}
+
+// flip mask over the 4 weak indices for candidate j (nibble tables, see scl_kernel.hip):
+// R1 {}, {i0}, {i1}, {i0,i1}; SPC even {}, {0,1}, {0,2}, {0,3}, {1,2}, {1,3}, {2,3},
+// {0,1,2,3}; SPC odd {0}, {1}, {2}, {3}, {0,1,2}, {0,1,3}, {0,2,3}, {1,2,3}.
+PCG_DEV uint32_t ls_flip_sel(uint32_t code, uint32_t j, uint32_t oddpar)
+{
+    const uint32_t tab = code == OP_S_R1 ? 0x3210u : oddpar ? 0xEDB78421u : 0xFCA69530u;
+    return (tab >> (4 * j)) & 0xFu;
+}
+
+// ---- path selection over the group ---------------------------------------------------
+// Candidates cv[0..K) of every active path (p < P), enumerated as e = p*K + j like the
+// reference's metric array.  Survivor q < np (descending metric, the order
+// simplePartialSortDescending leaves) is delivered to lane q of the group as
+// (val, src path, j).  Fast path: local sorting network + LP-lane merge rounds; if
+// any adjacent pair among the first lim+1 selected values is equal (the only case in
+// which the swap order shows), every group re-runs the literal selection sort.
+template <int K>
+PCG_DEV void cx_desc(float (&v)[8], uint32_t (&id)[8], int a, int b)
+{
+    const bool sw = v[b] > v[a];
+    const float va = v[a], vb = v[b];
+    const uint32_t ia = id[a], ib = id[b];
+    v[a] = sw ? vb : va;
+    v[b] = sw ? va : vb;
+    id[a] = sw ? ib : ia;
+    id[b] = sw ? ia : ib;
+}
+
+template <int K>
+PCG_DEV void local_sort(float (&v)[8], uint32_t (&id)[8])
+{
+    if constexpr (K == 2) {
+        cx_desc<K>(v, id, 0, 1);
+    } else if constexpr (K == 4) {
+        cx_desc<K>(v, id, 0, 1); cx_desc<K>(v, id, 2, 3);
+        cx_desc<K>(v, id, 0, 2); cx_desc<K>(v, id, 1, 3);
+        cx_desc<K>(v, id, 1, 2);
+    } else {
+        // 19-comparator network for 8 inputs
+        cx_desc<K>(v, id, 0, 2); cx_desc<K>(v, id, 1, 3); cx_desc<K>(v, id, 4, 6); cx_desc<K>(v, id, 5, 7);
+        cx_desc<K>(v, id, 0, 4); cx_desc<K>(v, id, 1, 5); cx_desc<K>(v, id, 2, 6); cx_desc<K>(v, id, 3, 7);
+        cx_desc<K>(v, id, 0, 1); cx_desc<K>(v, id, 2, 3); cx_desc<K>(v, id, 4, 5); cx_desc<K>(v, id, 6, 7);
+        cx_desc<K>(v, id, 2, 4); cx_desc<K>(v, id, 3, 5);
+        cx_desc<K>(v, id, 1, 4); cx_desc<K>(v, id, 3, 6);
+        cx_desc<K>(v, id, 1, 2); cx_desc<K>(v, id, 3, 4); cx_desc<K>(v, id, 5, 6);
+    }
+}
+
+template <int J>
+PCG_DEV void grp_max_step(float& v, uint32_t& code)
+{
+    const float ov = ubits(xpartner<J>(fbits(v)));
+    const uint32_t oc = xpartner<J>(code);
+    if (ov > v || (ov == v && oc < code)) {
+        v = ov;
+        code = oc;
+    }
+}
+
+template <int LP>
+PCG_DEV void grp_max(float& v, uint32_t& code)
+{
+    if constexpr (LP > 1) grp_max_step<1>(v, code);
+    if constexpr (LP > 2) grp_max_step<2>(v, code);
+    if constexpr (LP > 4) grp_max_step<4>(v, code);
+    if constexpr (LP > 8) grp_max_step<8>(v, code);
+    if constexpr (LP > 16) grp_max_step<16>(v, code);
+    if constexpr (LP > 32) grp_max_step<32>(v, code);
+}
+
+template <int LP, int K>
+PCG_DEV void ls_select(const Ls<LP>& c, const float (&cv)[8], uint32_t P, uint32_t np, float& val, uint32_t& src,
+                       uint32_t& jsel)
+{
+    const uint32_t C = P * K;
+    const bool act = c.p < P;
+    float v[8];
+    uint32_t id[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        v[j] = (act && j < K) ? cv[j] : -__builtin_inff();
+        id[j] = (uint32_t)j;
+    }
+    local_sort<K>(v, id);
+    const uint32_t R = C > np ? np + 1 : C;
+    float prev = 0.0f;
+    bool tie = false;
+    val = 0.0f;
+    src = 0;
+    jsel = 0;
+    for (uint32_t r = 0; r < R; ++r) {
+        float bv = v[0];
+        uint32_t code = (c.p << 3) | id[0];
+        grp_max<LP>(bv, code);
+        if (r > 0 && bv == prev)
+            tie = true;
+        prev = bv;
+        if (r < np && c.p == r) {
+            val = bv;
+            src = code >> 3;
+            jsel = code & 7u;
+        }
+        if ((code >> 3) == c.p) { // the winner pops its head
+#pragma unroll
+            for (int j = 0; j < K - 1; ++j) {
+                v[j] = v[j + 1];
+                id[j] = id[j + 1];
+            }
+            v[K - 1] = -__builtin_inff();
+        }
+    }
+    if (ballot(tie) == 0ull)
+        return;
+    // literal simplePartialSortDescending per group (rare: exact metric ties)
+    float* cval = c.lds + c.ly.cval + c.gb * 8u;
+    uint32_t* cid = reinterpret_cast<uint32_t*>(c.lds + c.ly.cid) + c.gb * 8u;
+    if (act) {
+#pragma unroll
+        for (uint32_t j = 0; j < K; ++j) {
+            cval[c.p * K + j] = cv[j];
+            cid[c.p * K + j] = c.p * K + j;
+        }
+    }
+    wsync();
+    if (c.p == 0) {
+        const uint32_t lim = (C - 1) < np ? (C - 1) : np;
+        for (uint32_t i = 0; i < lim; ++i) {
+            uint32_t b = i;
+            for (uint32_t j = i + 1; j < C; ++j)
+                if (cval[j] > cval[b])
+                    b = j;
+            const float tv = cval[i];
+            const uint32_t ti = cid[i];
+            cval[i] = cval[b];
+            cid[i] = cid[b];
+            cval[b] = tv;
+            cid[b] = ti;
+        }
+    }
+    wsync();
+    if (c.p < np) {
+        val = cval[c.p];
+        const uint32_t e = cid[c.p];
+        src = e / K;
+        jsel = e % K;
+    }
+    wsync();
+}
+
+// Duplicate the LDS path state of path `srcp` into this lane: slot table row and
+// codeword words [0, nw).  Converged code (bpermute); act = this lane survives.
+template <int LP>
+PCG_DEV void ls_dup(Ls<LP>& c, uint32_t srcp, uint32_t nw, bool act)
+{
+    const int sl = (int)(c.gb | srcp);
+    const uint32_t lo = shfl((uint32_t)c.ptr, sl), hi = shfl((uint32_t)(c.ptr >> 32), sl);
+    c.ptr = ((uint64_t)hi << 32) | lo;
+    const uint32_t* srow = c.row_of((uint32_t)sl);
+    uint32_t* row = c.row();
+    // one wave's LDS instructions execute in order: every lane's read of word w
+    // completes before any lane's write of word w
+    for (uint32_t w = 0; w < nw; ++w) {
+        const uint32_t x = srow[w << 6];
+        if (act)
+            row[w << 6] = x;
+    }
+}
+
+// ---- branching leaves at n >= 8 (Rate-1 :353-413, SPC :498-621) ----------------------
+template <int LP, typename Src>
+PCG_DEV void ls_branch_leaf(Ls<LP>& c, Src src, uint32_t code, uint32_t s, uint32_t o, uint32_t& P)
+{
+    const uint32_t n = 1u << s;
+    const uint32_t sl = s == c.top ? 0u : c.src_lane(s);
+    const uint32_t kk = code == OP_S_R1 ? 2u : 4u;
+    float T[4];
+    uint32_t I[4], par = 0;
+    if (n == 8) {
+        const float4 a = src.ld(0, sl), b = src.ld(1, sl);
+        const float v[8] = { a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w };
+        weak8(v, kk, T, I, par);
+    } else {
+        ls_weak(c, src, sl, n, kk, T, I, par);
+    }
+    float cv[8];
+    r1_spc_cands(code, c.m, T, par, cv);
+    float val;
+    uint32_t sp, j;
+    uint32_t np;
+    if (code == OP_S_R1) {
+        const uint32_t C = P * 4;
+        np = C < c.L ? C : c.L;
+        ls_select<LP, 4>(c, cv, P, np, val, sp, j);
+    } else {
+        const uint32_t C = P * 8;
+        np = C < c.L ? C : c.L;
+        ls_select<LP, 8>(c, cv, P, np, val, sp, j);
+    }
+    const bool surv = c.p < np;
+    // survivors take the source path's weak indices / parity and state
+    const int sln = (int)(c.gb | sp);
+    uint32_t Is[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+        Is[t] = shfl(I[t], sln);
+    const uint32_t pars = shfl(par, sln);
+    ls_dup(c, sp, (o + 31u) >> 5, surv);
+    P = np;
+    if (!surv)
+        return;
+    c.m = val;
+    const uint32_t fm = ls_flip_sel(code, j, pars & 0x80000000u ? 1u : 0u);
+    // hard decisions of the source path's leaf LLRs (its slot via the copied row)
+    const uint32_t sl2 = s == c.top ? 0u : c.src_lane(s);
+    uint32_t* row = c.row();
+    for (uint32_t w0 = 0; w0 < n; w0 += 32) {
+        const uint32_t nb = n < 32 ? n : 32u;
+        uint32_t word = 0;
+        for (uint32_t q = 0; q < nb / 4; ++q) {
+            const float4 x = src.ld((w0 >> 2) + q, sl2);
+            word |= ((fbits(x.x) >> 31) | ((fbits(x.y) >> 31) << 1) | ((fbits(x.z) >> 31) << 2) |
+                     ((fbits(x.w) >> 31) << 3))
+                    << (4u * q);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+            if (((fm >> t) & 1u) && Is[t] >= w0 && Is[t] < w0 + nb)
+                word ^= 1u << (Is[t] - w0);
+        const uint32_t pos = o + w0;
+        if (nb == 32) {
+            row[(pos >> 5) << 6] = word;
+        } else {
+            const uint32_t sh = pos & 31u, msk = ((1u << nb) - 1u) << sh;
+            uint32_t* wp = row + ((pos >> 5) << 6);
+            *wp = (*wp & ~msk) | (word << sh);
+        }
+    }
+}
+
+// ---- size-8 subtrees in registers (ShortRateRNode(8), scl_avx_float.cpp:273-307) -----
+struct LsSt8 {
+    float x8[8];
+    float a4[4];
+    uint32_t bits; // bit i = codeword position o + i
+    uint32_t root; // path index at subtree entry
+    uint32_t P;
+    bool branched;
+};
+
+PCG_DEV float ordered8(const float (&a)[8])
+{
+    return a[0] + a[1] + a[2] + a[3] + a[4] + a[5] + a[6] + a[7];
+}
+
+// candidates of a leaf of size n (2 or 4) on v[0..n): cv[0..k) and per-candidate n-bit
+// patterns packed 4 bits each into pat (REP :428-481, R1 :365-379, SPC :511-585).
+PCG_DEV void st_cands8(uint32_t kind, const float (&v)[4], uint32_t n, float m, float (&cv)[8], uint32_t& pat)
+{
+    const uint32_t nmask = (1u << n) - 1u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        cv[j] = 0.0f;
+    if (kind == ST_REP) { // zero padded to 8 lanes
+        float z[8], o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float l = j < (int)n && j < 4 ? v[j & 3] : 0.0f;
+            z[j] = 0.0f + minps(l, 0.0f);
+            o[j] = 0.0f + maxps(l, 0.0f);
+        }
+        cv[0] = m + ordered8(z);
+        cv[1] = m - ordered8(o);
+        pat = nmask << 4;
+        return;
+    }
+    float T[4];
+    uint32_t I[4], base = 0, par = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        T[j] = fabs_(v[j]);
+        I[j] = (uint32_t)j;
+        if (j < (int)n) {
+            par ^= fbits(v[j]);
+            base |= (fbits(v[j]) >> 31) << j;
+        }
+    }
+    const uint32_t kk = kind == ST_R1 ? 2u : 4u;
+    const uint32_t lim = (n - 1) < kk ? (n - 1) : kk;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        if (t < (int)lim) {
+            float bv = T[t];
+            uint32_t b = (uint32_t)t;
+#pragma unroll
+            for (int j = t + 1; j < 4; ++j) {
+                const bool better = j < (int)n && T[j] < bv;
+                bv = better ? T[j] : bv;
+                b = better ? (uint32_t)j : b;
+            }
+            const uint32_t tv = fbits(T[t]), ti = I[t];
+            uint32_t bi = I[t];
+#pragma unroll
+            for (int j = t + 1; j < 4; ++j) {
+                const uint32_t mj = 0u - (uint32_t)(b == (uint32_t)j);
+                bi = (I[j] & mj) | (bi & ~mj);
+                T[j] = ubits((tv & mj) | (fbits(T[j]) & ~mj));
+                I[j] = (ti & mj) | (I[j] & ~mj);
+            }
+            T[t] = bv;
+            I[t] = bi;
+        }
+    }
+    const uint32_t ib[4] = { 1u << I[0], 1u << I[1], 1u << I[2], 1u << I[3] };
+    if (kind == ST_R1) {
+        cv[0] = m;
+        cv[1] = m - T[0];
+        cv[2] = m - T[1];
+        cv[3] = m - T[0] - T[1];
+        pat = base | ((base ^ ib[0]) << 4) | ((base ^ ib[1]) << 8) | ((base ^ ib[0] ^ ib[1]) << 12);
+        return;
+    }
+    const bool odd = (par & 0x80000000u) != 0;
+    float mm = m, pinv = 1.0f;
+    if (odd) {
+        pinv = 0.0f;
+        mm -= T[0];
+    }
+    cv[0] = mm;
+    cv[1] = mm - pinv * T[0] - T[1];
+    cv[2] = mm - pinv * T[0] - T[2];
+    cv[3] = mm - pinv * T[0] - T[3];
+    cv[4] = mm - T[1] - T[2];
+    cv[5] = mm - T[1] - T[3];
+    cv[6] = mm - T[2] - T[3];
+    cv[7] = mm - pinv * T[0] - T[1] - T[2] - T[3];
+    pat = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        const uint32_t fm = ls_flip_sel(OP_S_SPC, j, odd ? 1u : 0u);
+        uint32_t fl = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q)
+            fl |= ((fm >> q) & 1u) ? ib[q] : 0u;
+        pat |= ((base ^ fl) & nmask) << (4 * j);
+    }
+}
+
+template <int LP>
+PCG_DEV void st8_r0(Ls<LP>& c, const float (&v)[4], uint32_t n)
+{
+    float q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        q[j] = 0.0f + minps(j < (int)n && j < 4 ? v[j & 3] : 0.0f, 0.0f);
+    c.m = c.m + ordered8(q);
+}
+
+template <int LP>
+PCG_DEV void st8_branch(Ls<LP>& c, LsSt8& st, uint32_t kind, const float (&v)[4], uint32_t n, uint32_t boff)
+{
+    float cv[8];
+    uint32_t pat = 0;
+    st_cands8(kind, v, n, c.m, cv, pat);
+    float val;
+    uint32_t sp, j, np;
+    if (kind == ST_R1) {
+        const uint32_t C = st.P * 4;
+        np = C < c.L ? C : c.L;
+        ls_select<LP, 4>(c, cv, st.P, np, val, sp, j);
+    } else if (kind == ST_SPC) {
+        const uint32_t C = st.P * 8;
+        np = C < c.L ? C : c.L;
+        ls_select<LP, 8>(c, cv, st.P, np, val, sp, j);
+    } else {
+        const uint32_t C = st.P * 2;
+        np = C < c.L ? C : c.L;
+        ls_select<LP, 2>(c, cv, st.P, np, val, sp, j);
+    }
+    const int sl = (int)(c.gb | sp);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        st.x8[i] = shfl(st.x8[i], sl);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        st.a4[i] = shfl(st.a4[i], sl);
+    st.bits = shfl(st.bits, sl);
+    st.root = shfl(st.root, sl);
+    pat = shfl(pat, sl);
+    st.bits |= ((pat >> (4 * j)) & ((1u << n) - 1u)) << boff;
+    c.m = val;
+    st.P = np;
+    st.branched = true;
+}
+
+template <int LP>
+PCG_DEV void st8_child2(Ls<LP>& c, LsSt8& st, uint32_t kind, const float (&a2)[4], uint32_t boff)
+{
+    if (kind == ST_R0)
+        st8_r0(c, a2, 2);
+    else
+        st8_branch(c, st, kind, a2, 2, boff);
+}
+
+template <int LP>
+PCG_DEV void st8_child4(Ls<LP>& c, LsSt8& st, uint32_t d, uint32_t boff)
+{
+    const uint32_t kind = d & 7u;
+    if (kind == ST_R0) {
+        st8_r0(c, st.a4, 4);
+    } else if (kind != ST_RATER) {
+        const float v[4] = { st.a4[0], st.a4[1], st.a4[2], st.a4[3] };
+        st8_branch(c, st, kind, v, 4, boff);
+    } else { // ShortRateRNode(4): F, left(2), G, right(2), CombineBitsShort
+        float a2[4] = { polar_f(st.a4[0], st.a4[2]), polar_f(st.a4[1], st.a4[3]), 0.0f, 0.0f };
+        st8_child2(c, st, (d >> 3) & 3u, a2, boff);
+        a2[0] = polar_g(st.a4[0], st.a4[2], ((st.bits >> boff) & 1u) << 31);
+        a2[1] = polar_g(st.a4[1], st.a4[3], ((st.bits >> (boff + 1)) & 1u) << 31);
+        st8_child2(c, st, (d >> 5) & 3u, a2, boff + 2);
+        st.bits ^= ((st.bits >> (boff + 2)) & 3u) << boff;
+    }
+}
+
+template <int LP, typename Src>
+PCG_DEV void ls_st8(Ls<LP>& c, Src src, uint32_t desc, uint32_t o, uint32_t& P)
+{
+    LsSt8 st;
+    st.P = P;
+    st.branched = false;
+    st.root = c.p;
+    st.bits = 0;
+    {
+        const uint32_t sl = c.top == 3 ? 0u : c.src_lane(3);
+        const float4 lo = src.ld(0, sl), hi = src.ld(1, sl);
+        st.x8[0] = lo.x; st.x8[1] = lo.y; st.x8[2] = lo.z; st.x8[3] = lo.w;
+        st.x8[4] = hi.x; st.x8[5] = hi.y; st.x8[6] = hi.z; st.x8[7] = hi.w;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        st.a4[i] = polar_f(st.x8[i], st.x8[i + 4]);
+    st8_child4(c, st, desc & 0xffu, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        st.a4[i] = polar_g(st.x8[i], st.x8[i + 4], ((st.bits >> i) & 1u) << 31);
+    st8_child4(c, st, (desc >> 8) & 0xffu, 4);
+    st.bits ^= (st.bits >> 4) & 0xFu; // CombineBitsShort(4)
+    // write back the 8 bits at [o, o+8); after branching, first take the LDS path
+    // state (slot table, codeword prefix) of the path each survivor descends from
+    const uint32_t sh = o & 31u, wo = o >> 5, msk = 0xFFu << sh;
+    if (st.branched)
+        ls_dup(c, st.root, wo + 1, c.p < st.P);
+    P = st.P;
+    if (c.p < P) {
+        uint32_t* w = c.row() + (wo << 6);
+        *w = (*w & ~msk) | (st.bits << sh);
+    }
+}
+
+// ---- the kernel ------------------------------------------------------------------------
+template <int LP>
+__global__ void __launch_bounds__(64) sclls_kernel(KernelArgs a)
+{
+    extern __shared__ float smem[];
+    constexpr uint32_t G = 64 / LP;
+    Ls<LP> c;
+    c.lds = smem;
+    c.N = a.N;
+    c.L = a.L;
+    c.top = a.log2N;
+    c.Sl = a.lds_stage_limit;
+    c.ly = ls_layout(a.N, a.lds_stage_limit);
+    c.lane = threadIdx.x;
+    c.p = c.lane & (LP - 1);
+    c.gb = c.lane & ~(uint32_t)(LP - 1);
+    c.gs = a.scratch ? a.scratch + (uint64_t)blockIdx.x * a.scratch_floats : nullptr;
+    const uint32_t W = a.N >= 32 ? a.N / 32 : 1u;
+
+    for (uint64_t fb = (uint64_t)blockIdx.x * G; fb < a.F; fb += (uint64_t)gridDim.x * G) {
+        const uint64_t frame = fb + c.lane / LP;
+        const bool fvalid = frame < a.F;
+        c.y = a.llr + (fvalid ? frame : a.F - 1) * a.N;
+        c.m = 0.0f; // a freshly constructed decoder
+        c.ptr = 0;
+        uint32_t P = 1;
+        for (uint32_t kop = 0; kop < a.nops; ++kop) {
+            const uint32_t w = ld_const(a.ops, kop);
+            const uint32_t code = op_code(w), s = op_stage(w), o = op_off(w);
+            const bool act = c.p < P;
+            switch (code) {
+            case OP_F:
+                ls_fg_op<OP_F>(c, s, o, act);
+                break;
+            case OP_G:
+                ls_fg_op<OP_G>(c, s, o, act);
+                break;
+            case OP_COMB:
+                ls_comb(c, s, o, act);
+                break;
+            case OP_S_ST8: {
+                const uint32_t desc = ld_const(a.ops, ++kop);
+                with_stage(c, 3, [&](auto src) { ls_st8(c, src, desc, o, P); });
+                break;
+            }
+            case OP_S_R0:
+                with_stage(c, s, [&](auto src) { ls_r0(c, src, s, o, act); });
+                break;
+            default: // OP_S_R1 / OP_S_SPC (n >= 8)
+                with_stage(c, s, [&](auto src) { ls_branch_leaf(c, src, code, s, o, P); });
+                break;
+            }
+            wsync();
+        }
+        // extractBestPath (scl_avx_float.cpp:711-750): first path in list order whose
+        // detector check passes, else path 0.
+        const bool act = c.p < P;
+        uint32_t* row = c.row();
+        if (!a.systematic && act) {
+            for (uint32_t wi = 0; wi < W; ++wi)
+                row[wi << 6] = transform_word(row[wi << 6], a.N);
+            for (uint32_t d = 1; d < W; d <<= 1)
+                for (uint32_t wi = 0; wi < W; ++wi)
+                    if (!(wi & d))
+                        row[wi << 6] ^= row[(wi + d) << 6];
+        }
+        uint32_t syn = a.crc_c0;
+        {
+            uint32_t cw = ~0u, word = 0;
+            for (uint32_t idx = 0; idx < a.K; ++idx) {
+                const uint32_t pos = ld_const(reinterpret_cast<const uint32_t*>(a.info_pos), idx >> 1);
+                const uint32_t ps = (idx & 1u) ? (pos >> 16) : (pos & 0xffffu);
+                if ((ps >> 5) != cw) {
+                    cw = ps >> 5;
+                    word = row[cw << 6];
+                }
+                if ((word >> (ps & 31u)) & 1u)
+                    syn ^= ld_const(a.crc_m, idx);
+            }
+        }
+        const uint64_t okm = ballot(act && syn == 0u);
+        const uint32_t gm = (uint32_t)((okm >> c.gb) & (LP == 64 ? ~0ull : ((1ull << LP) - 1ull)));
+        const uint32_t chosen = gm ? (uint32_t)__builtin_ctz(gm) : 0u;
+        const uint32_t* crow = c.row_of(c.gb | chosen);
+        if (fvalid) {
+            for (uint32_t b = c.p; b < a.kb; b += LP) {
+                uint32_t byte = 0;
+                for (uint32_t j = 0; j < 8; ++j) {
+                    const uint32_t idx = 8 * b + j;
+                    if (idx < a.K) {
+                        const uint32_t ps = a.info_pos[idx];
+                        byte |= ((crow[(ps >> 5) << 6] >> (ps & 31u)) & 1u) << (7 - j);
+                    }
+                }
+                a.info[frame * a.kb + b] = (uint8_t)byte;
+            }
+            if (c.p == 0 && a.ok)
+                a.ok[frame] = gm ? 1 : 0;
+            if (a.metrics && c.p < a.L)
+                a.metrics[frame * a.L + c.p] = act ? c.m : 0.0f;
+        }
+        wsync();
+    }
+}
+
+} // namespace
+
+int sclls_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* lds_stage_limit,
+                 uint64_t* scratch_floats)
+{
+    if (L < 2 || L > 32 || N < 8)
+        return -4;
+    const uint32_t top = (uint32_t)__builtin_ctz(N);
+    if (top > 3 + 12) // 5-bit slot fields for stages 3 .. top-1 in 64 bits
+        return -4;
+    uint32_t budget = 40 * 1024 / 4; // floats per wave
+    if (const char* e = getenv("PCG_SCL_LDS_KB"))
+        budget = (uint32_t)atoi(e) * 1024 / 4;
+    uint32_t Sl = top;
+    while (Sl > LS_MINS && ls_layout(N, Sl).total > budget)
+        --Sl;
+    if (const char* e = getenv("PCG_SCL_STAGE_LIMIT")) {
+        const uint32_t v = (uint32_t)atoi(e);
+        if (v >= LS_MINS && v <= top)
+            Sl = v;
+    }
+    const LsLayout ly = ls_layout(N, Sl);
+    if (ly.total * 4 > 160 * 1024)
+        return -4;
+    *wave_lds_floats = ly.total;
+    *lds_stage_limit = Sl;
+    *scratch_floats = Sl < top ? 64ull * ((1ull << top) - (1ull << Sl)) : 0ull;
+    return 0;
+}
+
+static uint32_t lp_of(uint32_t L)
+{
+    uint32_t lp = 2;
+    while (lp < L)
+        lp <<= 1;
+    return lp;
+}
+
+uint64_t sclls_units(uint64_t F, uint32_t L, uint32_t wave_lds_floats)
+{
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    uint64_t wpc = (160ull * 1024) / ((uint64_t)wave_lds_floats * 4);
+    if (wpc < 1)
+        wpc = 1;
+    if (wpc > 16)
+        wpc = 16;
+    if (const char* e = getenv("PCG_SCL_WPC"))
+        wpc = (uint64_t)atoi(e);
+    const uint64_t G = 64 / lp_of(L);
+    const uint64_t need = (F + G - 1) / G;
+    const uint64_t cap = (uint64_t)cus * wpc;
+    return need < cap ? need : cap;
+}
+
+int launch_sclls(const KernelArgs& a, hipStream_t stream)
+{
+    const uint64_t grid = sclls_units(a.F, a.L, a.wave_lds_floats);
+    if (grid == 0)
+        return 0;
+    const size_t lds = (size_t)a.wave_lds_floats * sizeof(float);
+    switch (lp_of(a.L)) {
+    case 2: hipLaunchKernelGGL(sclls_kernel<2>, dim3((uint32_t)grid), dim3(64), lds, stream, a); break;
+    case 4: hipLaunchKernelGGL(sclls_kernel<4>, dim3((uint32_t)grid), dim3(64), lds, stream, a); break;
+    case 8: hipLaunchKernelGGL(sclls_kernel<8>, dim3((uint32_t)grid), dim3(64), lds, stream, a); break;
+    case 16: hipLaunchKernelGGL(sclls_kernel<16>, dim3((uint32_t)grid), dim3(64), lds, stream, a); break;
+    case 32: hipLaunchKernelGGL(sclls_kernel<32>, dim3((uint32_t)grid), dim3(64), lds, stream, a); break;
+    default: return -4;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+} // namespace pcg

@@ -19,6 +19,14 @@ PCG_DEV void wsync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Read-only schedule words through the constant address space: uniform indices then
+// become scalar loads (s_load, scalar cache) instead of vector loads on every op.
+typedef const __attribute__((address_space(4))) uint32_t cu32_t;
+PCG_DEV uint32_t ld_const(const uint32_t* p, uint32_t i)
+{
+    return reinterpret_cast<cu32_t*>(reinterpret_cast<uintptr_t>(p))[i];
+}
+
 PCG_DEV uint32_t fbits(float x) { return __float_as_uint(x); }
 PCG_DEV float ubits(uint32_t u) { return __uint_as_float(u); }
 PCG_DEV uint32_t sgn(float x) { return __float_as_uint(x) & 0x80000000u; }

@@ -43,7 +43,7 @@ if os.environ.get("PCG_OPPROF"):
     _native.lib().pcg_dev_opprof_fetch(buf)
     names = {1: "F", 2: "G", 3: "G0", 4: "COMB", 5: "COPY0", 6: "RONE", 16: "L_R0", 17: "L_R1", 18: "L_REP", 19: "L_SPC",
              20: "L_DREP", 21: "L_DSPC", 22: "L_DSPC8", 23: "L_TREP", 24: "L_TYPE5", 25: "L_REPR1", 26: "L_ZSPC8",
-             27: "L_ZSPC", 40: "S_R0", 41: "S_R1", 42: "S_REP", 43: "S_SPC",
+             27: "L_ZSPC", 40: "S_R0", 41: "S_R1", 42: "S_REP", 43: "S_SPC", 44: "S_ST8",
              48: "~weak", 49: "~cand", 50: "~sort", 51: "~commit"}
     tot = sum(buf[2 * c] for c in range(48))
     frames_done = a.F * (a.reps + 3)
