@@ -123,33 +123,57 @@ PCG_DEV void with_stage(const Ls<LP>& c, uint32_t s, Fn&& fn)
         fn(lds_st(c, s));
 }
 
+// ---- streaming helpers ---------------------------------------------------------------
+// Loads of a batch of U float4 chunks are all issued before any is used; loops below
+// prefetch batch b+1 while batch b is processed (ping-pong), so a lane keeps up to
+// 2U chunk loads in flight instead of exposing one memory latency per iteration.
+template <int U, typename Src>
+PCG_DEV void ld_batch(const Src& src, uint32_t c0, uint32_t nq, uint32_t sl, float4 (&x)[U])
+{
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (c0 + u < nq)
+            x[u] = src.ld(c0 + u, sl);
+}
+
+// Call fn(x, c0) on every batch of U chunks of [0, nq), batch b+1 loaded during b.
+template <int U, typename Src, typename Fn>
+PCG_DEV void stream(const Src& src, uint32_t nq, uint32_t sl, Fn&& fn)
+{
+    float4 xa[U], xb[U];
+    ld_batch<U>(src, 0, nq, sl, xa);
+    for (uint32_t c0 = 0; c0 < nq; c0 += 2 * U) {
+        if (c0 + U < nq)
+            ld_batch<U>(src, c0 + U, nq, sl, xb);
+        fn(xa, c0);
+        if (c0 + U < nq) {
+            if (c0 + 2 * U < nq)
+                ld_batch<U>(src, c0 + 2 * U, nq, sl, xa);
+            fn(xb, c0 + U);
+        }
+    }
+}
+
 // ---- F / G ---------------------------------------------------------------------------
 // alpha[s-1] of every active path from alpha[s] of its slot (avx_float.h:101-164),
-// h = 2^(s-1) >= 8 elements = hq float4 chunks; 4 chunks in flight per lane.
+// h = 2^(s-1) >= 8 elements = hq float4 chunks; both halves streamed ping-pong.
 template <int OPC, int LP, typename Src, typename Dst>
 PCG_DEV void ls_fg(const Ls<LP>& c, Src src, Dst dst, uint32_t s, uint32_t o, bool act)
 {
+    constexpr int U = 4;
     const uint32_t hq = 1u << (s - 3);
     const uint32_t sl = s == c.top ? 0u : c.src_lane(s);
     const uint32_t* row = c.row();
     if (!act)
         return;
-    for (uint32_t c0 = 0; c0 < hq; c0 += 4) {
-        float4 xa[4], xb[4];
-        uint32_t wb[4];
-#pragma unroll
-        for (uint32_t u = 0; u < 4; ++u) {
-            if (c0 + u < hq) {
-                xa[u] = src.ld(c0 + u, sl);
-                xb[u] = src.ld(c0 + u + hq, sl);
-                if (OPC == OP_G) {
-                    const uint32_t i = o + 4u * (c0 + u);
-                    wb[u] = row[(i >> 5) << 6] >> (i & 31u);
-                }
-            }
+    auto body = [&](const float4 (&xa)[U], const float4 (&xb)[U], uint32_t c0) {
+        uint32_t wb = 0;
+        if (OPC == OP_G) {
+            const uint32_t i = o + 4u * c0; // 4U = 16 elements share one bit word
+            wb = row[(i >> 5) << 6] >> (i & 31u);
         }
 #pragma unroll
-        for (uint32_t u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
             if (c0 + u < hq) {
                 float4 r;
                 if (OPC == OP_F) {
@@ -158,13 +182,31 @@ PCG_DEV void ls_fg(const Ls<LP>& c, Src src, Dst dst, uint32_t s, uint32_t o, bo
                     r.z = polar_f(xa[u].z, xb[u].z);
                     r.w = polar_f(xa[u].w, xb[u].w);
                 } else {
-                    r.x = polar_g(xa[u].x, xb[u].x, (wb[u] & 1u) << 31);
-                    r.y = polar_g(xa[u].y, xb[u].y, ((wb[u] >> 1) & 1u) << 31);
-                    r.z = polar_g(xa[u].z, xb[u].z, ((wb[u] >> 2) & 1u) << 31);
-                    r.w = polar_g(xa[u].w, xb[u].w, ((wb[u] >> 3) & 1u) << 31);
+                    const uint32_t bq = wb >> (4 * u);
+                    r.x = polar_g(xa[u].x, xb[u].x, (bq & 1u) << 31);
+                    r.y = polar_g(xa[u].y, xb[u].y, ((bq >> 1) & 1u) << 31);
+                    r.z = polar_g(xa[u].z, xb[u].z, ((bq >> 2) & 1u) << 31);
+                    r.w = polar_g(xa[u].w, xb[u].w, ((bq >> 3) & 1u) << 31);
                 }
                 dst.st(c0 + u, r);
             }
+        }
+    };
+    float4 a0[U], b0[U], a1[U], b1[U];
+    ld_batch<U>(src, 0, hq, sl, a0);
+    ld_batch<U>(src, hq, 2 * hq, sl, b0);
+    for (uint32_t c0 = 0; c0 < hq; c0 += 2 * U) {
+        if (c0 + U < hq) {
+            ld_batch<U>(src, c0 + U, hq, sl, a1);
+            ld_batch<U>(src, hq + c0 + U, 2 * hq, sl, b1);
+        }
+        body(a0, b0, c0);
+        if (c0 + U < hq) {
+            if (c0 + 2 * U < hq) {
+                ld_batch<U>(src, c0 + 2 * U, hq, sl, a0);
+                ld_batch<U>(src, hq + c0 + 2 * U, 2 * hq, sl, b0);
+            }
+            body(a1, b1, c0 + U);
         }
     }
 }
@@ -223,17 +265,22 @@ PCG_DEV void ls_r0(Ls<LP>& c, Src src, uint32_t s, uint32_t o, bool act)
     if (!act)
         return;
     float acc[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
-    for (uint32_t q = 0; q < nq; q += 2) {
-        const float4 a = src.ld(q, sl), b = src.ld(q + 1, sl);
-        acc[0] = acc[0] + minps(a.x, 0.0f);
-        acc[1] = acc[1] + minps(a.y, 0.0f);
-        acc[2] = acc[2] + minps(a.z, 0.0f);
-        acc[3] = acc[3] + minps(a.w, 0.0f);
-        acc[4] = acc[4] + minps(b.x, 0.0f);
-        acc[5] = acc[5] + minps(b.y, 0.0f);
-        acc[6] = acc[6] + minps(b.z, 0.0f);
-        acc[7] = acc[7] + minps(b.w, 0.0f);
-    }
+    stream<4>(src, nq, sl, [&](const float4 (&x)[4], uint32_t c0) {
+#pragma unroll
+        for (int u = 0; u < 4; u += 2) {
+            if (c0 + u < nq) { // chunks come in pairs (nq even): one 8-float AVX vector
+                const float4 a = x[u], b = x[u + 1];
+                acc[0] = acc[0] + minps(a.x, 0.0f);
+                acc[1] = acc[1] + minps(a.y, 0.0f);
+                acc[2] = acc[2] + minps(a.z, 0.0f);
+                acc[3] = acc[3] + minps(a.w, 0.0f);
+                acc[4] = acc[4] + minps(b.x, 0.0f);
+                acc[5] = acc[5] + minps(b.y, 0.0f);
+                acc[6] = acc[6] + minps(b.z, 0.0f);
+                acc[7] = acc[7] + minps(b.w, 0.0f);
+            }
+        }
+    });
     float r = acc[0];
 #pragma unroll
     for (int j = 1; j < 8; ++j)
@@ -338,6 +385,63 @@ PCG_DEV void ls_weak(const Ls<LP>& c, Src src, uint32_t sl, uint32_t n, uint32_t
                 ovi[t] = it;
             }
         }
+    }
+}
+
+// One streaming pass for the same result when it is unambiguous: the lim+1 smallest
+// |llr| (stable insertion) with their indices, and the parity.  Pass t of the
+// reference picks the (t+1)-th smallest; only equal values among the first lim+1 make
+// its swap order observable -- then *tie is set and ls_weak runs instead.
+template <int LP, typename Src>
+PCG_DEV void weak_fast(Src src, uint32_t sl, uint32_t n, uint32_t kk, float (&T)[4], uint32_t (&I)[4],
+                       uint32_t& par, bool& tie)
+{
+    float sv[5];
+    uint32_t si[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+        sv[j] = __builtin_inff();
+        si[j] = ~0u;
+    }
+    uint32_t px = 0;
+    const bool r1 = kk == 2u; // keep 3 entries for Rate-1, 5 for SPC
+    stream<4>(src, n >> 2, sl, [&](const float4 (&x)[4], uint32_t c0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (c0 + u < (n >> 2)) {
+                const float xv[4] = { x[u].x, x[u].y, x[u].z, x[u].w };
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    px ^= fbits(xv[e]);
+                    float v = fabs_(xv[e]);
+                    uint32_t i = 4u * (c0 + u) + e;
+#pragma unroll
+                    for (int j = 0; j < 5; ++j) {
+                        if (j < 3 || !r1) {
+                            const bool lt = v < sv[j];
+                            const float tv = sv[j];
+                            const uint32_t ti = si[j];
+                            sv[j] = lt ? v : tv;
+                            si[j] = lt ? i : ti;
+                            v = lt ? tv : v;
+                            i = lt ? ti : i;
+                        }
+                    }
+                }
+            }
+        }
+    });
+    par = px;
+    bool t = false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        if ((uint32_t)j < kk)
+            t = t || sv[j] == sv[j + 1];
+    tie = t;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        T[j] = (uint32_t)j < kk ? sv[j] : 0.0f;
+        I[j] = (uint32_t)j < kk ? si[j] : (uint32_t)j;
     }
 }
 
@@ -592,7 +696,10 @@ PCG_DEV void ls_branch_leaf(Ls<LP>& c, Src src, uint32_t code, uint32_t s, uint3
         const float v[8] = { a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w };
         weak8(v, kk, T, I, par);
     } else {
-        ls_weak(c, src, sl, n, kk, T, I, par);
+        bool tie;
+        weak_fast<LP>(src, sl, n, kk, T, I, par, tie);
+        if (tie)
+            ls_weak(c, src, sl, n, kk, T, I, par);
     }
     float cv[8];
     r1_spc_cands(code, c.m, T, par, cv);
@@ -628,11 +735,16 @@ PCG_DEV void ls_branch_leaf(Ls<LP>& c, Src src, uint32_t code, uint32_t s, uint3
     for (uint32_t w0 = 0; w0 < n; w0 += 32) {
         const uint32_t nb = n < 32 ? n : 32u;
         uint32_t word = 0;
-        for (uint32_t q = 0; q < nb / 4; ++q) {
-            const float4 x = src.ld((w0 >> 2) + q, sl2);
-            word |= ((fbits(x.x) >> 31) | ((fbits(x.y) >> 31) << 1) | ((fbits(x.z) >> 31) << 2) |
-                     ((fbits(x.w) >> 31) << 3))
-                    << (4u * q);
+        float4 xq[8];
+        ld_batch<8>(src, w0 >> 2, (w0 + nb) >> 2, sl2, xq);
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) {
+            if (q < nb / 4) {
+                const float4 x = xq[q];
+                word |= ((fbits(x.x) >> 31) | ((fbits(x.y) >> 31) << 1) | ((fbits(x.z) >> 31) << 2) |
+                         ((fbits(x.w) >> 31) << 3))
+                        << (4u * q);
+            }
         }
 #pragma unroll
         for (int t = 0; t < 4; ++t)
@@ -982,7 +1094,7 @@ int sclls_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* ld
     const uint32_t top = (uint32_t)__builtin_ctz(N);
     if (top > 3 + 12) // 5-bit slot fields for stages 3 .. top-1 in 64 bits
         return -4;
-    uint32_t budget = 40 * 1024 / 4; // floats per wave
+    uint32_t budget = 20 * 1024 / 4; // floats per wave: occupancy beats LDS-resident stages
     if (const char* e = getenv("PCG_SCL_LDS_KB"))
         budget = (uint32_t)atoi(e) * 1024 / 4;
     uint32_t Sl = top;
