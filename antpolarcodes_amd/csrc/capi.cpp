@@ -19,6 +19,7 @@ struct pcg_plan {
     uint32_t* d_crc_m = nullptr;
     uint32_t wave_lds_floats = 0;
     uint32_t lds_stage_limit = 0;
+    uint32_t scl_virt = 0;
     uint64_t scratch_floats = 0;  // per scratch unit (codeword or lane-serial wave)
     float* d_scratch = nullptr;   // grown on demand
     uint64_t scratch_frames = 0;  // capacity in scratch units
@@ -126,7 +127,7 @@ int pcg_plan_create(pcg_plan** out,
         p->wave_lds_floats = pcg::sc_wave_lds_floats(N);
     } else {
         rc = p->host.scl_kind == 0
-                 ? pcg::sclls_layout(N, L, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats)
+                 ? pcg::sclls_layout(N, L, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats, &p->scl_virt)
                  : pcg::scl_layout(N, L, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats);
         if (rc != 0) {
             delete p;
@@ -157,7 +158,7 @@ int pcg_plan_create(pcg_plan** out,
     hipError_t e;
     if ((e = hipMalloc(&p->d_ops, 4 * std::max<size_t>(1, h.ops.size()))) != hipSuccess ||
         (e = hipMalloc(&p->d_info_pos, 2 * (h.info_pos.size() + 2))) != hipSuccess ||
-        (e = hipMalloc(&p->d_crc_m, 4 * std::max<size_t>(1, h.crc_m.size()))) != hipSuccess) {
+        (e = hipMalloc(&p->d_crc_m, 4 * (h.crc_m.size() + h.crc_rows.size() + 1))) != hipSuccess) {
         free_plan_device(p);
         delete p;
         return hip_fail(e, "hipMalloc(plan)");
@@ -167,7 +168,10 @@ int pcg_plan_create(pcg_plan** out,
          (e = hipMemcpy(p->d_info_pos, h.info_pos.data(), 2 * h.info_pos.size(), hipMemcpyHostToDevice)) !=
              hipSuccess) ||
         (!h.crc_m.empty() &&
-         (e = hipMemcpy(p->d_crc_m, h.crc_m.data(), 4 * h.crc_m.size(), hipMemcpyHostToDevice)) != hipSuccess)) {
+         (e = hipMemcpy(p->d_crc_m, h.crc_m.data(), 4 * h.crc_m.size(), hipMemcpyHostToDevice)) != hipSuccess) ||
+        (!h.crc_rows.empty() &&
+         (e = hipMemcpy(p->d_crc_m + h.crc_m.size(), h.crc_rows.data(), 4 * h.crc_rows.size(),
+                        hipMemcpyHostToDevice)) != hipSuccess)) {
         free_plan_device(p);
         delete p;
         return hip_fail(e, "hipMemcpy(plan)");
@@ -222,6 +226,8 @@ int pcg_decode_f32(pcg_plan* p,
     a.L = h.L;
     a.info_pos = p->d_info_pos;
     a.crc_m = p->d_crc_m;
+    a.crc_bits = (uint32_t)h.crc_kind;
+    a.crc_rows = p->d_crc_m + h.crc_m.size();
     a.crc_c0 = h.crc_c0;
     a.systematic = h.systematic;
     a.info = info;
@@ -229,6 +235,7 @@ int pcg_decode_f32(pcg_plan* p,
     a.metrics = metrics;
     a.wave_lds_floats = p->wave_lds_floats;
     a.lds_stage_limit = p->lds_stage_limit;
+    a.scl_virt = p->scl_virt;
     a.scratch_floats = p->scratch_floats;
     if (getenv("PCG_OPPROF")) {
         if (!g_prof && hipMalloc(&g_prof, 128 * sizeof(unsigned long long)) == hipSuccess)

@@ -14,6 +14,8 @@ struct KernelArgs {
     const uint16_t* info_pos; // K info positions (device)
     const uint32_t* crc_m;    // K syndrome columns (device)
     uint32_t crc_c0;
+    uint32_t crc_bits;        // 0, 8, 16, 32
+    const uint32_t* crc_rows; // crc_bits x W codeword masks (device): syndrome bit r = c0_r ^ parity(cw & row r)
     int systematic;
     uint8_t* info;            // F x kb (device)
     uint8_t* ok;              // F or null
@@ -24,6 +26,7 @@ struct KernelArgs {
     uint32_t lds_stage_limit; // SCL: stages < limit live in LDS
     unsigned long long* prof; // dev-only: per-op-code [cycles, count] (null = off)
     uint32_t flags;           // dev-only experiment switches (PCG_FLAGS), 0 in production
+    uint32_t scl_virt;        // lane-serial SCL: top stages recomputed instead of stored (0..2)
 };
 
 // LDS floats one SC codeword needs: alpha (N floats, index 0 unused) + packed bits.
@@ -43,7 +46,7 @@ uint64_t scl_scratch_frames(uint64_t F);
 // lane-serial SCL kernel (sclls_kernel.hip): per-wave LDS / scratch layout, the
 // number of scratch units (waves) a launch of F frames uses, and the launch
 int sclls_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* lds_stage_limit,
-                 uint64_t* scratch_floats);
+                 uint64_t* scratch_floats, uint32_t* virt);
 uint64_t sclls_units(uint64_t F, uint32_t L, uint32_t wave_lds_floats);
 int launch_sclls(const KernelArgs& a, hipStream_t stream);
 } // namespace pcg

@@ -260,6 +260,25 @@ int build_plan(PlanHost& p,
         crc_syndrome(crc_kind, msg.data(), (int)kb, &s);
         p.crc_m[j] = s ^ s0;
     }
+    // the same model in codeword coordinates: row r marks the info positions whose
+    // column has syndrome bit r set
+    {
+        const uint32_t W = N >= 32 ? N / 32 : 1;
+        const uint32_t cb = (uint32_t)crc_kind;
+        const uint32_t hi = cb >= 32 ? 0u : ~((1u << cb) - 1u);
+        bool narrow = (p.crc_c0 & hi) == 0;
+        for (uint32_t j = 0; j < K; ++j)
+            narrow = narrow && (p.crc_m[j] & hi) == 0;
+        if (!narrow) {
+            *err = "internal: detector syndrome wider than its check bits";
+            return -4;
+        }
+        p.crc_rows.assign((size_t)cb * W, 0u);
+        for (uint32_t j = 0; j < K; ++j)
+            for (uint32_t r = 0; r < cb; ++r)
+                if ((p.crc_m[j] >> r) & 1u)
+                    p.crc_rows[r * W + (p.info_pos[j] >> 5)] |= 1u << (p.info_pos[j] & 31u);
+    }
     // self-check of the affine model on random messages
     std::mt19937 rng(12345);
     for (int t = 0; t < 8 && K > 0; ++t) {

@@ -69,6 +69,7 @@ struct PlanHost {
     std::vector<uint16_t> info_pos; // K non-frozen positions, ascending (bitcontainer.cpp:68-84)
     std::vector<uint32_t> crc_m;    // K affine syndrome columns
     uint32_t crc_c0 = 0;            // syndrome of the all-zero message
+    std::vector<uint32_t> crc_rows; // crc_kind x W codeword-position masks of the same model
     uint32_t node_count = 0;
     std::vector<int> node_types;    // pre-order census (op code of each node; 0 = internal)
     bool scl_st8 = true;            // emit lane-serial size-8 subtrees for SCL

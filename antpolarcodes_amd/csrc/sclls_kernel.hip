@@ -29,6 +29,7 @@
 #include "plan.hpp"
 #include "wave.hpp"
 
+#include <stdio.h>
 #include <stdlib.h>
 
 namespace pcg {
@@ -41,10 +42,27 @@ constexpr uint32_t LS_MINS = 3; // lowest memory stage: size-8 nodes
 struct LsLayout {
     uint32_t alpha; // 64 * (2^Sl - 8) floats (stages [3, Sl))
     uint32_t bits;  // 64 * W words
-    uint32_t cval;  // 64 * 8 floats: tie fallback candidate list
-    uint32_t cid;   // 64 * 8 words
     uint32_t total;
 };
+
+// Stage top-1 (the root's children) is never stored: it is recomputed from the
+// channel LLRs and the path's own left-half bits wherever it is read (RootSt), which
+// removes the largest per-path buffers and their HBM traffic.  Memory stages are
+// [3, mtop) with mtop = top-1 (or 3 when N = 8: no memory stage at all).
+// With virt = 2 stage top-2 is recomputed as well (from four channel LLRs).
+__host__ __device__ inline uint32_t ls_mtop(uint32_t top, uint32_t virt)
+{
+    const uint32_t m = top - virt;
+    return m > 3u ? m : 3u;
+}
+__host__ __device__ inline uint32_t ls_max_virt(uint32_t top) { return top >= 4 ? 1u : 0u; }
+
+// Global scratch slab of one wave: alpha stages [Sl, mtop), then the tie-fallback
+// candidate list (64 * 8 values + 64 * 8 ids; rarely touched, so not worth LDS).
+__host__ __device__ inline uint64_t ls_gl_alpha_floats(uint32_t mt, uint32_t Sl)
+{
+    return Sl < mt ? 64ull * ((1ull << mt) - (1ull << Sl)) : 0ull;
+}
 
 __host__ __device__ inline LsLayout ls_layout(uint32_t N, uint32_t Sl)
 {
@@ -54,10 +72,6 @@ __host__ __device__ inline LsLayout ls_layout(uint32_t N, uint32_t Sl)
     o += Sl > LS_MINS ? 64u * ((1u << Sl) - 8u) : 0u;
     y.bits = o;
     o += 64u * (N >= 32 ? N / 32 : 1u);
-    y.cval = o;
-    o += 512;
-    y.cid = o;
-    o += 512;
     y.total = o;
     return y;
 }
@@ -68,7 +82,7 @@ struct Ls {
     float* lds;
     float* gs;        // this wave's global scratch slab
     const float* y;   // this lane's codeword channel LLRs
-    uint32_t N, L, top, Sl;
+    uint32_t N, L, top, Sl, mt; // mt: first recomputed stage (stages >= mt are never stored)
     LsLayout ly;
     uint32_t lane, p, gb; // lane, path index in the group, group base lane
     uint64_t ptr;         // slot of stage s at bits 5(s-3)
@@ -95,9 +109,67 @@ struct GlSt {
     PCG_DEV float4 ld(uint32_t c, uint32_t l) const { return *reinterpret_cast<const float4*>(b + ((uint64_t)((c << 6) + l)) * 4u); }
     PCG_DEV void st(uint32_t c, const float4& v) const { *reinterpret_cast<float4*>(b + ((uint64_t)((c << 6) + lane)) * 4u) = v; }
 };
+// Stages >= mt are never stored.  With virt = 1 the root's children (stage top-1)
+// are recomputed wherever they are read: the left child F(y_j, y_j+N/2) is path
+// independent (it is only used before any branching), the right child
+// G(y_j, y_j+N/2, bit_j) uses the path's own left-half codeword bits, which every
+// survivor inherits unchanged.
+PCG_DEV float4 f4_f(const float4& a, const float4& b)
+{
+    return make_float4(polar_f(a.x, b.x), polar_f(a.y, b.y), polar_f(a.z, b.z), polar_f(a.w, b.w));
+}
+PCG_DEV float4 f4_g(const float4& a, const float4& b, uint32_t wb)
+{
+    return make_float4(polar_g(a.x, b.x, (wb & 1u) << 31), polar_g(a.y, b.y, ((wb >> 1) & 1u) << 31),
+                       polar_g(a.z, b.z, ((wb >> 2) & 1u) << 31), polar_g(a.w, b.w, ((wb >> 3) & 1u) << 31));
+}
+
 struct ChSt { // the channel LLRs of the lane's own codeword (stage top)
     const float* y;
     PCG_DEV float4 ld(uint32_t c, uint32_t) const { return reinterpret_cast<const float4*>(y)[c]; }
+};
+template <bool LEFT>
+struct RootSt { // stage top-1, left or right child of the root
+    const float* y;
+    const uint32_t* row; // the lane's bit row (word w at [w*64])
+    uint32_t hq1;        // N/8 chunks: distance of y_j+N/2
+    PCG_DEV float4 ld(uint32_t c, uint32_t) const
+    {
+        const float4 a = reinterpret_cast<const float4*>(y)[c];
+        const float4 b = reinterpret_cast<const float4*>(y)[c + hq1];
+        if (LEFT)
+            return f4_f(a, b);
+        const uint32_t i = 4u * c;
+        return f4_g(a, b, row[(i >> 5) << 6] >> (i & 31u));
+    }
+};
+// Any recomputed stage behind one wave-uniform switch (leaves and size-8 subtrees at
+// stage top or top-1: rare, so one instantiation serves all of them).
+struct VirtSt {
+    const float* y;
+    const uint32_t* row;
+    uint32_t hq1;
+    bool root, left;
+    PCG_DEV float4 ld(uint32_t c, uint32_t l) const
+    {
+        if (!root)
+            return ChSt{ y }.ld(c, l);
+        return left ? RootSt<true>{ y, row, hq1 }.ld(c, l) : RootSt<false>{ y, row, hq1 }.ld(c, l);
+    }
+};
+
+// prefetch depth (float4 chunks per batch) of the streaming loops for a storage
+template <typename S>
+struct Pre {
+    static constexpr int U = 4;
+};
+template <bool LEFT>
+struct Pre<RootSt<LEFT>> {
+    static constexpr int U = 2;
+};
+template <>
+struct Pre<VirtSt> {
+    static constexpr int U = 2;
 };
 
 template <int LP>
@@ -111,12 +183,12 @@ PCG_DEV GlSt gl_st(const Ls<LP>& c, uint32_t s)
     return GlSt{ c.gs + 64ull * ((1ull << s) - (1ull << c.Sl)), c.lane };
 }
 
-// Run fn with the storage of stage s (wave-uniform choice).
+// Run fn with the storage of stage s for a node at offset o (wave-uniform choice).
 template <int LP, typename Fn>
-PCG_DEV void with_stage(const Ls<LP>& c, uint32_t s, Fn&& fn)
+PCG_DEV void with_stage(const Ls<LP>& c, uint32_t s, uint32_t o, Fn&& fn)
 {
-    if (s == c.top)
-        fn(ChSt{ c.y });
+    if (s >= c.mt)
+        fn(VirtSt{ c.y, c.row(), c.N >> 3, s != c.top, o < (c.N >> 1) });
     else if (s >= c.Sl)
         fn(gl_st(c, s));
     else
@@ -124,9 +196,10 @@ PCG_DEV void with_stage(const Ls<LP>& c, uint32_t s, Fn&& fn)
 }
 
 // ---- streaming helpers ---------------------------------------------------------------
-// Loads of a batch of U float4 chunks are all issued before any is used; loops below
-// prefetch batch b+1 while batch b is processed (ping-pong), so a lane keeps up to
-// 2U chunk loads in flight instead of exposing one memory latency per iteration.
+// All loads of a batch are issued before any is used, and batch b+1 is loaded while
+// batch b is processed (ping-pong).  Chunk counts are powers of two: small ones are
+// one guarded batch pair; large ones run whole pairs with no guards (the last
+// prefetch wraps to chunk 0), so the compiler can keep counted vmcnt waits.
 template <int U, typename Src>
 PCG_DEV void ld_batch(const Src& src, uint32_t c0, uint32_t nq, uint32_t sl, float4 (&x)[U])
 {
@@ -135,79 +208,84 @@ PCG_DEV void ld_batch(const Src& src, uint32_t c0, uint32_t nq, uint32_t sl, flo
         if (c0 + u < nq)
             x[u] = src.ld(c0 + u, sl);
 }
+template <int U, typename Src>
+PCG_DEV void ld_full(const Src& src, uint32_t c0, uint32_t sl, float4 (&x)[U])
+{
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        x[u] = src.ld(c0 + u, sl);
+}
 
-// Call fn(x, c0) on every batch of U chunks of [0, nq), batch b+1 loaded during b.
+// fn(x, c0, valid): chunks c0 .. c0+valid-1 of [0, nq) in x[0..valid).
 template <int U, typename Src, typename Fn>
 PCG_DEV void stream(const Src& src, uint32_t nq, uint32_t sl, Fn&& fn)
 {
     float4 xa[U], xb[U];
-    ld_batch<U>(src, 0, nq, sl, xa);
+    if (nq <= 2 * U) {
+        ld_batch<U>(src, 0, nq, sl, xa);
+        ld_batch<U>(src, U, nq, sl, xb);
+        fn(xa, 0u, nq < (uint32_t)U ? nq : (uint32_t)U);
+        if (nq > (uint32_t)U)
+            fn(xb, (uint32_t)U, nq - U);
+        return;
+    }
+    ld_full<U>(src, 0, sl, xa);
     for (uint32_t c0 = 0; c0 < nq; c0 += 2 * U) {
-        if (c0 + U < nq)
-            ld_batch<U>(src, c0 + U, nq, sl, xb);
-        fn(xa, c0);
-        if (c0 + U < nq) {
-            if (c0 + 2 * U < nq)
-                ld_batch<U>(src, c0 + 2 * U, nq, sl, xa);
-            fn(xb, c0 + U);
-        }
+        ld_full<U>(src, c0 + U, sl, xb);
+        fn(xa, c0, (uint32_t)U);
+        ld_full<U>(src, (c0 + 2 * U) & (nq - 1), sl, xa);
+        fn(xb, c0 + U, (uint32_t)U);
     }
 }
 
 // ---- F / G ---------------------------------------------------------------------------
 // alpha[s-1] of every active path from alpha[s] of its slot (avx_float.h:101-164),
-// h = 2^(s-1) >= 8 elements = hq float4 chunks; both halves streamed ping-pong.
+// h = 2^(s-1) >= 8 elements = hq float4 chunks (a power of two >= 2); the two halves
+// are streamed together.
 template <int OPC, int LP, typename Src, typename Dst>
 PCG_DEV void ls_fg(const Ls<LP>& c, Src src, Dst dst, uint32_t s, uint32_t o, bool act)
 {
-    constexpr int U = 4;
+    constexpr int U = Pre<Src>::U;
     const uint32_t hq = 1u << (s - 3);
-    const uint32_t sl = s == c.top ? 0u : c.src_lane(s);
+    const uint32_t sl = c.src_lane(s);
     const uint32_t* row = c.row();
     if (!act)
         return;
-    auto body = [&](const float4 (&xa)[U], const float4 (&xb)[U], uint32_t c0) {
+    auto body = [&](const float4 (&xa)[U], const float4 (&xb)[U], uint32_t c0, uint32_t valid) {
         uint32_t wb = 0;
         if (OPC == OP_G) {
-            const uint32_t i = o + 4u * c0; // 4U = 16 elements share one bit word
+            const uint32_t i = o + 4u * c0; // the batch's 4U <= 16 elements share a bit word
             wb = row[(i >> 5) << 6] >> (i & 31u);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (c0 + u < hq) {
-                float4 r;
-                if (OPC == OP_F) {
-                    r.x = polar_f(xa[u].x, xb[u].x);
-                    r.y = polar_f(xa[u].y, xb[u].y);
-                    r.z = polar_f(xa[u].z, xb[u].z);
-                    r.w = polar_f(xa[u].w, xb[u].w);
-                } else {
-                    const uint32_t bq = wb >> (4 * u);
-                    r.x = polar_g(xa[u].x, xb[u].x, (bq & 1u) << 31);
-                    r.y = polar_g(xa[u].y, xb[u].y, ((bq >> 1) & 1u) << 31);
-                    r.z = polar_g(xa[u].z, xb[u].z, ((bq >> 2) & 1u) << 31);
-                    r.w = polar_g(xa[u].w, xb[u].w, ((bq >> 3) & 1u) << 31);
-                }
+            if ((uint32_t)u < valid) {
+                const float4 r = OPC == OP_F ? f4_f(xa[u], xb[u]) : f4_g(xa[u], xb[u], wb >> (4 * u));
                 dst.st(c0 + u, r);
             }
         }
     };
     float4 a0[U], b0[U], a1[U], b1[U];
-    ld_batch<U>(src, 0, hq, sl, a0);
-    ld_batch<U>(src, hq, 2 * hq, sl, b0);
+    if (hq <= 2 * U) {
+        ld_batch<U>(src, 0, hq, sl, a0);
+        ld_batch<U>(src, hq, 2 * hq, sl, b0);
+        ld_batch<U>(src, U, hq, sl, a1);
+        ld_batch<U>(src, hq + U, 2 * hq, sl, b1);
+        body(a0, b0, 0u, hq < (uint32_t)U ? hq : (uint32_t)U);
+        if (hq > (uint32_t)U)
+            body(a1, b1, (uint32_t)U, hq - U);
+        return;
+    }
+    ld_full<U>(src, 0, sl, a0);
+    ld_full<U>(src, hq, sl, b0);
     for (uint32_t c0 = 0; c0 < hq; c0 += 2 * U) {
-        if (c0 + U < hq) {
-            ld_batch<U>(src, c0 + U, hq, sl, a1);
-            ld_batch<U>(src, hq + c0 + U, 2 * hq, sl, b1);
-        }
-        body(a0, b0, c0);
-        if (c0 + U < hq) {
-            if (c0 + 2 * U < hq) {
-                ld_batch<U>(src, c0 + 2 * U, hq, sl, a0);
-                ld_batch<U>(src, hq + c0 + 2 * U, 2 * hq, sl, b0);
-            }
-            body(a1, b1, c0 + U);
-        }
+        ld_full<U>(src, c0 + U, sl, a1);
+        ld_full<U>(src, hq + c0 + U, sl, b1);
+        body(a0, b0, c0, (uint32_t)U);
+        const uint32_t nx = (c0 + 2 * U) & (hq - 1);
+        ld_full<U>(src, nx, sl, a0);
+        ld_full<U>(src, hq + nx, sl, b0);
+        body(a1, b1, c0 + U, (uint32_t)U);
     }
 }
 
@@ -215,10 +293,24 @@ template <int OPC, int LP>
 PCG_DEV void ls_fg_op(Ls<LP>& c, uint32_t s, uint32_t o, bool act)
 {
     const uint32_t d = s - 1;
+    if (d >= c.mt) // recomputed where it is read
+        return;
+    auto run = [&](auto dst) {
+        if (s == c.top)
+            ls_fg<OPC>(c, ChSt{ c.y }, dst, s, o, act);
+        else if (s >= c.mt && o < (c.N >> 1))
+            ls_fg<OPC>(c, RootSt<true>{ c.y, c.row(), c.N >> 3 }, dst, s, o, act);
+        else if (s >= c.mt)
+            ls_fg<OPC>(c, RootSt<false>{ c.y, c.row(), c.N >> 3 }, dst, s, o, act);
+        else if (s >= c.Sl)
+            ls_fg<OPC>(c, gl_st(c, s), dst, s, o, act);
+        else
+            ls_fg<OPC>(c, lds_st(c, s), dst, s, o, act);
+    };
     if (d >= c.Sl)
-        with_stage(c, s, [&](auto src) { ls_fg<OPC>(c, src, gl_st(c, d), s, o, act); });
+        run(gl_st(c, d));
     else
-        with_stage(c, s, [&](auto src) { ls_fg<OPC>(c, src, lds_st(c, d), s, o, act); });
+        run(lds_st(c, d));
     c.own(d);
 }
 
@@ -265,10 +357,11 @@ PCG_DEV void ls_r0(Ls<LP>& c, Src src, uint32_t s, uint32_t o, bool act)
     if (!act)
         return;
     float acc[8] = { 0, 0, 0, 0, 0, 0, 0, 0 };
-    stream<4>(src, nq, sl, [&](const float4 (&x)[4], uint32_t c0) {
+    constexpr int U = Pre<Src>::U; // even
+    stream<U>(src, nq, sl, [&](const float4 (&x)[U], uint32_t c0, uint32_t valid) {
 #pragma unroll
-        for (int u = 0; u < 4; u += 2) {
-            if (c0 + u < nq) { // chunks come in pairs (nq even): one 8-float AVX vector
+        for (int u = 0; u < U; u += 2) {
+            if ((uint32_t)u < valid) { // chunks come in pairs (nq, valid even): one 8-float vector
                 const float4 a = x[u], b = x[u + 1];
                 acc[0] = acc[0] + minps(a.x, 0.0f);
                 acc[1] = acc[1] + minps(a.y, 0.0f);
@@ -405,10 +498,11 @@ PCG_DEV void weak_fast(Src src, uint32_t sl, uint32_t n, uint32_t kk, float (&T)
     }
     uint32_t px = 0;
     const bool r1 = kk == 2u; // keep 3 entries for Rate-1, 5 for SPC
-    stream<4>(src, n >> 2, sl, [&](const float4 (&x)[4], uint32_t c0) {
+    constexpr int U = Pre<Src>::U;
+    stream<U>(src, n >> 2, sl, [&](const float4 (&x)[U], uint32_t c0, uint32_t valid) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (c0 + u < (n >> 2)) {
+        for (int u = 0; u < U; ++u) {
+            if ((uint32_t)u < valid) {
                 const float xv[4] = { x[u].x, x[u].y, x[u].z, x[u].w };
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -628,8 +722,8 @@ PCG_DEV void ls_select(const Ls<LP>& c, const float (&cv)[8], uint32_t P, uint32
     if (ballot(tie) == 0ull)
         return;
     // literal simplePartialSortDescending per group (rare: exact metric ties)
-    float* cval = c.lds + c.ly.cval + c.gb * 8u;
-    uint32_t* cid = reinterpret_cast<uint32_t*>(c.lds + c.ly.cid) + c.gb * 8u;
+    float* cval = c.gs + ls_gl_alpha_floats(c.mt, c.Sl) + c.gb * 8u;
+    uint32_t* cid = reinterpret_cast<uint32_t*>(cval + 512);
     if (act) {
 #pragma unroll
         for (uint32_t j = 0; j < K; ++j) {
@@ -673,9 +767,21 @@ PCG_DEV void ls_dup(Ls<LP>& c, uint32_t srcp, uint32_t nw, bool act)
     c.ptr = ((uint64_t)hi << 32) | lo;
     const uint32_t* srow = c.row_of((uint32_t)sl);
     uint32_t* row = c.row();
-    // one wave's LDS instructions execute in order: every lane's read of word w
-    // completes before any lane's write of word w
-    for (uint32_t w = 0; w < nw; ++w) {
+    // one wave's LDS instructions execute in order: every lane's read of a word
+    // completes before any lane's write of it; 8 reads are issued before their writes
+    uint32_t w = 0;
+    for (; w + 8 <= nw; w += 8) {
+        uint32_t x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            x[u] = srow[(w + u) << 6];
+        if (act) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                row[(w + u) << 6] = x[u];
+        }
+    }
+    for (; w < nw; ++w) {
         const uint32_t x = srow[w << 6];
         if (act)
             row[w << 6] = x;
@@ -735,12 +841,14 @@ PCG_DEV void ls_branch_leaf(Ls<LP>& c, Src src, uint32_t code, uint32_t s, uint3
     for (uint32_t w0 = 0; w0 < n; w0 += 32) {
         const uint32_t nb = n < 32 ? n : 32u;
         uint32_t word = 0;
-        float4 xq[8];
-        ld_batch<8>(src, w0 >> 2, (w0 + nb) >> 2, sl2, xq);
+        constexpr int UB = 2 * Pre<Src>::U; // chunks loaded together
+        float4 xq[UB];
 #pragma unroll
         for (uint32_t q = 0; q < 8; ++q) {
+            if (q % UB == 0)
+                ld_batch<UB>(src, (w0 >> 2) + q, (w0 + nb) >> 2, sl2, xq);
             if (q < nb / 4) {
-                const float4 x = xq[q];
+                const float4 x = xq[q % UB];
                 word |= ((fbits(x.x) >> 31) | ((fbits(x.y) >> 31) << 1) | ((fbits(x.z) >> 31) << 2) |
                          ((fbits(x.w) >> 31) << 3))
                         << (4u * q);
@@ -979,23 +1087,58 @@ PCG_DEV void ls_st8(Ls<LP>& c, Src src, uint32_t desc, uint32_t o, uint32_t& P)
     }
 }
 
+// ---- CRC check of a path's codeword (the plan's GF(2) syndrome model) -----------------
+// The syndrome of the info bits is affine in them (plan.cpp); in codeword coordinates
+// bit r of it is c0_r ^ parity(sum_w popcount(word_w & rows[r][w])): W * CB and +
+// popcount pairs per lane, the masks wave-uniform scalar loads.
+template <int CB>
+PCG_DEV uint32_t crc_syn(const uint32_t* row, const uint32_t* rows, uint32_t W, uint32_t c0)
+{
+    uint32_t acc[CB];
+#pragma unroll
+    for (int r = 0; r < CB; ++r)
+        acc[r] = 0;
+    for (uint32_t w = 0; w < W; ++w) {
+        const uint32_t word = row[w << 6];
+#pragma unroll
+        for (int r = 0; r < CB; ++r)
+            acc[r] += (uint32_t)__builtin_popcount(word & ld_const(rows, r * W + w));
+    }
+    uint32_t syn = c0;
+#pragma unroll
+    for (int r = 0; r < CB; ++r)
+        syn ^= (acc[r] & 1u) << r;
+    return syn;
+}
+
 // ---- the kernel ------------------------------------------------------------------------
+#ifndef PCG_LS_MINW
+#define PCG_LS_MINW 2
+#endif
 template <int LP>
-__global__ void __launch_bounds__(64) sclls_kernel(KernelArgs a)
+__global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
 {
     extern __shared__ float smem[];
     constexpr uint32_t G = 64 / LP;
     Ls<LP> c;
     c.lds = smem;
+#ifdef PCG_LS_PROF
+    uint64_t* lprof = reinterpret_cast<uint64_t*>(smem + a.wave_lds_floats);
+    if (threadIdx.x == 0)
+        for (int b = 0; b < 64; ++b)
+            lprof[b] = 0;
+    wsync();
+#endif
     c.N = a.N;
     c.L = a.L;
     c.top = a.log2N;
     c.Sl = a.lds_stage_limit;
+    c.mt = ls_mtop(c.top, a.scl_virt);
     c.ly = ls_layout(a.N, a.lds_stage_limit);
     c.lane = threadIdx.x;
     c.p = c.lane & (LP - 1);
     c.gb = c.lane & ~(uint32_t)(LP - 1);
-    c.gs = a.scratch ? a.scratch + (uint64_t)blockIdx.x * a.scratch_floats : nullptr;
+    c.gs = a.scratch + (uint64_t)blockIdx.x * a.scratch_floats;
     const uint32_t W = a.N >= 32 ? a.N / 32 : 1u;
 
     for (uint64_t fb = (uint64_t)blockIdx.x * G; fb < a.F; fb += (uint64_t)gridDim.x * G) {
@@ -1005,10 +1148,16 @@ __global__ void __launch_bounds__(64) sclls_kernel(KernelArgs a)
         c.m = 0.0f; // a freshly constructed decoder
         c.ptr = 0;
         uint32_t P = 1;
+#ifdef PCG_LS_PROF
+        const uint64_t tf0 = __builtin_amdgcn_s_memtime();
+#endif
         for (uint32_t kop = 0; kop < a.nops; ++kop) {
             const uint32_t w = ld_const(a.ops, kop);
             const uint32_t code = op_code(w), s = op_stage(w), o = op_off(w);
             const bool act = c.p < P;
+#ifdef PCG_LS_PROF
+            const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
             switch (code) {
             case OP_F:
                 ls_fg_op<OP_F>(c, s, o, act);
@@ -1021,18 +1170,31 @@ __global__ void __launch_bounds__(64) sclls_kernel(KernelArgs a)
                 break;
             case OP_S_ST8: {
                 const uint32_t desc = ld_const(a.ops, ++kop);
-                with_stage(c, 3, [&](auto src) { ls_st8(c, src, desc, o, P); });
+                with_stage(c, 3, o, [&](auto src) { ls_st8(c, src, desc, o, P); });
                 break;
             }
             case OP_S_R0:
-                with_stage(c, s, [&](auto src) { ls_r0(c, src, s, o, act); });
+                with_stage(c, s, o, [&](auto src) { ls_r0(c, src, s, o, act); });
                 break;
             default: // OP_S_R1 / OP_S_SPC (n >= 8)
-                with_stage(c, s, [&](auto src) { ls_branch_leaf(c, src, code, s, o, P); });
+                with_stage(c, s, o, [&](auto src) { ls_branch_leaf(c, src, code, s, o, P); });
                 break;
             }
             wsync();
+#ifdef PCG_LS_PROF
+            {
+                const uint64_t t1 = __builtin_amdgcn_s_memtime();
+                uint32_t b = code;
+                if (code == OP_F || code == OP_G)
+                    b += s >= c.mt ? 16u : s >= c.Sl ? 8u : (s - 1 >= c.Sl ? 24u : 0u);
+                if (c.lane == 0)
+                    lprof[b] += t1 - t0;
+            }
+#endif
         }
+#ifdef PCG_LS_PROF
+        const uint64_t tf1 = __builtin_amdgcn_s_memtime();
+#endif
         // extractBestPath (scl_avx_float.cpp:711-750): first path in list order whose
         // detector check passes, else path 0.
         const bool act = c.p < P;
@@ -1045,19 +1207,13 @@ __global__ void __launch_bounds__(64) sclls_kernel(KernelArgs a)
                     if (!(wi & d))
                         row[wi << 6] ^= row[(wi + d) << 6];
         }
-        uint32_t syn = a.crc_c0;
-        {
-            uint32_t cw = ~0u, word = 0;
-            for (uint32_t idx = 0; idx < a.K; ++idx) {
-                const uint32_t pos = ld_const(reinterpret_cast<const uint32_t*>(a.info_pos), idx >> 1);
-                const uint32_t ps = (idx & 1u) ? (pos >> 16) : (pos & 0xffffu);
-                if ((ps >> 5) != cw) {
-                    cw = ps >> 5;
-                    word = row[cw << 6];
-                }
-                if ((word >> (ps & 31u)) & 1u)
-                    syn ^= ld_const(a.crc_m, idx);
-            }
+        // detector syndrome: bit r = c0_r ^ parity(codeword & row mask r)
+        uint32_t syn;
+        switch (a.crc_bits) {
+        case 8: syn = crc_syn<8>(row, a.crc_rows, W, a.crc_c0); break;
+        case 16: syn = crc_syn<16>(row, a.crc_rows, W, a.crc_c0); break;
+        case 32: syn = crc_syn<32>(row, a.crc_rows, W, a.crc_c0); break;
+        default: syn = a.crc_c0; break;
         }
         const uint64_t okm = ballot(act && syn == 0u);
         const uint32_t gm = (uint32_t)((okm >> c.gb) & (LP == 64 ? ~0ull : ((1ull << LP) - 1ull)));
@@ -1081,13 +1237,28 @@ __global__ void __launch_bounds__(64) sclls_kernel(KernelArgs a)
                 a.metrics[frame * a.L + c.p] = act ? c.m : 0.0f;
         }
         wsync();
+#ifdef PCG_LS_PROF
+        if (c.lane == 0) {
+            const uint64_t tf2 = __builtin_amdgcn_s_memtime();
+            lprof[60] += tf2 - tf1; // extractBestPath + output
+            lprof[61] += tf2 - tf0; // whole codeword group
+            lprof[62] += 1;
+        }
+#endif
     }
+#ifdef PCG_LS_PROF
+    wsync();
+    if (c.lane == 0 && a.prof)
+        for (int b = 0; b < 64; ++b)
+            if (lprof[b])
+                atomicAdd(&a.prof[b], (unsigned long long)lprof[b]);
+#endif
 }
 
 } // namespace
 
 int sclls_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* lds_stage_limit,
-                 uint64_t* scratch_floats)
+                 uint64_t* scratch_floats, uint32_t* virt)
 {
     if (L < 2 || L > 32 || N < 8)
         return -4;
@@ -1097,12 +1268,18 @@ int sclls_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* ld
     uint32_t budget = 20 * 1024 / 4; // floats per wave: occupancy beats LDS-resident stages
     if (const char* e = getenv("PCG_SCL_LDS_KB"))
         budget = (uint32_t)atoi(e) * 1024 / 4;
-    uint32_t Sl = top;
+    uint32_t vt = ls_max_virt(top);
+    if (const char* e = getenv("PCG_SCL_VIRT")) {
+        const uint32_t v = (uint32_t)atoi(e);
+        vt = v < vt ? v : vt;
+    }
+    const uint32_t mt = ls_mtop(top, vt);
+    uint32_t Sl = mt;
     while (Sl > LS_MINS && ls_layout(N, Sl).total > budget)
         --Sl;
     if (const char* e = getenv("PCG_SCL_STAGE_LIMIT")) {
         const uint32_t v = (uint32_t)atoi(e);
-        if (v >= LS_MINS && v <= top)
+        if (v >= LS_MINS && v <= mt)
             Sl = v;
     }
     const LsLayout ly = ls_layout(N, Sl);
@@ -1110,7 +1287,8 @@ int sclls_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* ld
         return -4;
     *wave_lds_floats = ly.total;
     *lds_stage_limit = Sl;
-    *scratch_floats = Sl < top ? 64ull * ((1ull << top) - (1ull << Sl)) : 0ull;
+    *scratch_floats = ls_gl_alpha_floats(mt, Sl) + 1024;
+    *virt = vt;
     return 0;
 }
 
@@ -1122,18 +1300,39 @@ static uint32_t lp_of(uint32_t L)
     return lp;
 }
 
+template <int LP>
+static int ls_resident(uint32_t lds_bytes)
+{
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, sclls_kernel<LP>, 64, lds_bytes) != hipSuccess)
+        n = 0;
+    return n;
+}
+
+// Waves (= scratch units) for a launch of F frames: one persistent wave per resident
+// slot (hipOccupancy: VGPR / LDS limits), capped at PCG_SCL_WPC waves per CU.
 uint64_t sclls_units(uint64_t F, uint32_t L, uint32_t wave_lds_floats)
 {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess)
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    uint64_t wpc = (160ull * 1024) / ((uint64_t)wave_lds_floats * 4);
-    if (wpc < 1)
-        wpc = 1;
-    if (wpc > 16)
-        wpc = 16;
+    const uint32_t lds = wave_lds_floats * 4u;
+    int res = 0;
+    switch (lp_of(L)) {
+    case 2: res = ls_resident<2>(lds); break;
+    case 4: res = ls_resident<4>(lds); break;
+    case 8: res = ls_resident<8>(lds); break;
+    case 16: res = ls_resident<16>(lds); break;
+    default: res = ls_resident<32>(lds); break;
+    }
+    uint64_t wpc = res > 0 ? (uint64_t)res : 1;
+    if (wpc > 8)
+        wpc = 8;
     if (const char* e = getenv("PCG_SCL_WPC"))
         wpc = (uint64_t)atoi(e);
+    if (getenv("PCG_DEBUG_OCC"))
+        fprintf(stderr, "[pcg] sclls: lds %u B, resident %d waves/CU, using %llu\n", lds, res,
+                (unsigned long long)wpc);
     const uint64_t G = 64 / lp_of(L);
     const uint64_t need = (F + G - 1) / G;
     const uint64_t cap = (uint64_t)cus * wpc;
@@ -1145,7 +1344,10 @@ int launch_sclls(const KernelArgs& a, hipStream_t stream)
     const uint64_t grid = sclls_units(a.F, a.L, a.wave_lds_floats);
     if (grid == 0)
         return 0;
-    const size_t lds = (size_t)a.wave_lds_floats * sizeof(float);
+    size_t lds = (size_t)a.wave_lds_floats * sizeof(float);
+#ifdef PCG_LS_PROF
+    lds += 64 * sizeof(uint64_t);
+#endif
     switch (lp_of(a.L)) {
     case 2: hipLaunchKernelGGL(sclls_kernel<2>, dim3((uint32_t)grid), dim3(64), lds, stream, a); break;
     case 4: hipLaunchKernelGGL(sclls_kernel<4>, dim3((uint32_t)grid), dim3(64), lds, stream, a); break;
