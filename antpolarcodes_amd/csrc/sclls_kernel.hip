@@ -87,6 +87,20 @@ struct Ls {
     uint32_t lane, p, gb; // lane, path index in the group, group base lane
     uint64_t ptr;         // slot of stage s at bits 5(s-3)
     float m;              // path metric
+#ifdef PCG_LS_PROF
+    uint64_t* lprof;
+    PCG_DEV void stamp(uint32_t b, uint64_t t0) const
+    {
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        if (lane == 0)
+            lprof[b] += t1 - t0;
+    }
+#define LS_T0() const uint64_t _t0 = __builtin_amdgcn_s_memtime()
+#define LS_STAMP(c, b) (c).stamp((b), _t0)
+#else
+#define LS_T0() (void)0
+#define LS_STAMP(c, b) (void)0
+#endif
     PCG_DEV uint32_t src_lane(uint32_t s) const { return gb | (uint32_t)((ptr >> (5u * (s - LS_MINS))) & 31u); }
     PCG_DEV void own(uint32_t s) { // alpha[s] of this path is now in its own lane
         const uint32_t sh = 5u * (s - LS_MINS);
@@ -624,103 +638,104 @@ PCG_DEV uint32_t ls_flip_sel(uint32_t code, uint32_t j, uint32_t oddpar)
 // (val, src path, j).  Fast path: local sorting network + LP-lane merge rounds; if
 // any adjacent pair among the first lim+1 selected values is equal (the only case in
 // which the swap order shows), every group re-runs the literal selection sort.
-template <int K>
-PCG_DEV void cx_desc(float (&v)[8], uint32_t (&id)[8], int a, int b)
+// Candidates travel as 64-bit keys: the float's order-preserving integer image above
+// ~code (code = path << 3 | j), so one unsigned compare orders by value and makes
+// every key unique.  -0 and +0 get different keys; they compare equal as floats, so
+// such a pair is caught by the tie test like any other equal pair.
+PCG_DEV uint32_t ord_of(float v)
 {
-    const bool sw = v[b] > v[a];
-    const float va = v[a], vb = v[b];
-    const uint32_t ia = id[a], ib = id[b];
-    v[a] = sw ? vb : va;
-    v[b] = sw ? va : vb;
-    id[a] = sw ? ib : ia;
-    id[b] = sw ? ia : ib;
+    const uint32_t u = fbits(v);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+PCG_DEV float val_of(uint32_t o) { return ubits((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o); }
+
+PCG_DEV void cx_desc(uint64_t (&k)[8], int a, int b)
+{
+    const uint64_t ka = k[a], kb = k[b];
+    const bool sw = kb > ka;
+    k[a] = sw ? kb : ka;
+    k[b] = sw ? ka : kb;
 }
 
 template <int K>
-PCG_DEV void local_sort(float (&v)[8], uint32_t (&id)[8])
+PCG_DEV void local_sort(uint64_t (&k)[8])
 {
     if constexpr (K == 2) {
-        cx_desc<K>(v, id, 0, 1);
+        cx_desc(k, 0, 1);
     } else if constexpr (K == 4) {
-        cx_desc<K>(v, id, 0, 1); cx_desc<K>(v, id, 2, 3);
-        cx_desc<K>(v, id, 0, 2); cx_desc<K>(v, id, 1, 3);
-        cx_desc<K>(v, id, 1, 2);
+        cx_desc(k, 0, 1); cx_desc(k, 2, 3);
+        cx_desc(k, 0, 2); cx_desc(k, 1, 3);
+        cx_desc(k, 1, 2);
     } else {
         // 19-comparator network for 8 inputs
-        cx_desc<K>(v, id, 0, 2); cx_desc<K>(v, id, 1, 3); cx_desc<K>(v, id, 4, 6); cx_desc<K>(v, id, 5, 7);
-        cx_desc<K>(v, id, 0, 4); cx_desc<K>(v, id, 1, 5); cx_desc<K>(v, id, 2, 6); cx_desc<K>(v, id, 3, 7);
-        cx_desc<K>(v, id, 0, 1); cx_desc<K>(v, id, 2, 3); cx_desc<K>(v, id, 4, 5); cx_desc<K>(v, id, 6, 7);
-        cx_desc<K>(v, id, 2, 4); cx_desc<K>(v, id, 3, 5);
-        cx_desc<K>(v, id, 1, 4); cx_desc<K>(v, id, 3, 6);
-        cx_desc<K>(v, id, 1, 2); cx_desc<K>(v, id, 3, 4); cx_desc<K>(v, id, 5, 6);
+        cx_desc(k, 0, 2); cx_desc(k, 1, 3); cx_desc(k, 4, 6); cx_desc(k, 5, 7);
+        cx_desc(k, 0, 4); cx_desc(k, 1, 5); cx_desc(k, 2, 6); cx_desc(k, 3, 7);
+        cx_desc(k, 0, 1); cx_desc(k, 2, 3); cx_desc(k, 4, 5); cx_desc(k, 6, 7);
+        cx_desc(k, 2, 4); cx_desc(k, 3, 5);
+        cx_desc(k, 1, 4); cx_desc(k, 3, 6);
+        cx_desc(k, 1, 2); cx_desc(k, 3, 4); cx_desc(k, 5, 6);
     }
 }
 
 template <int J>
-PCG_DEV void grp_max_step(float& v, uint32_t& code)
+PCG_DEV void kmax_step(uint64_t& k)
 {
-    const float ov = ubits(xpartner<J>(fbits(v)));
-    const uint32_t oc = xpartner<J>(code);
-    if (ov > v || (ov == v && oc < code)) {
-        v = ov;
-        code = oc;
-    }
+    const uint32_t lo = xpartner<J>((uint32_t)k), hi = xpartner<J>((uint32_t)(k >> 32));
+    const uint64_t o = ((uint64_t)hi << 32) | lo;
+    k = o > k ? o : k;
 }
 
 template <int LP>
-PCG_DEV void grp_max(float& v, uint32_t& code)
+PCG_DEV void grp_kmax(uint64_t& k)
 {
-    if constexpr (LP > 1) grp_max_step<1>(v, code);
-    if constexpr (LP > 2) grp_max_step<2>(v, code);
-    if constexpr (LP > 4) grp_max_step<4>(v, code);
-    if constexpr (LP > 8) grp_max_step<8>(v, code);
-    if constexpr (LP > 16) grp_max_step<16>(v, code);
-    if constexpr (LP > 32) grp_max_step<32>(v, code);
+    if constexpr (LP > 1) kmax_step<1>(k);
+    if constexpr (LP > 2) kmax_step<2>(k);
+    if constexpr (LP > 4) kmax_step<4>(k);
+    if constexpr (LP > 8) kmax_step<8>(k);
+    if constexpr (LP > 16) kmax_step<16>(k);
+    if constexpr (LP > 32) kmax_step<32>(k);
 }
 
 template <int LP, int K>
 PCG_DEV void ls_select(const Ls<LP>& c, const float (&cv)[8], uint32_t P, uint32_t np, float& val, uint32_t& src,
                        uint32_t& jsel)
 {
+    LS_T0();
     const uint32_t C = P * K;
     const bool act = c.p < P;
-    float v[8];
-    uint32_t id[8];
+    uint64_t k[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        v[j] = (act && j < K) ? cv[j] : -__builtin_inff();
-        id[j] = (uint32_t)j;
+        const uint32_t code = (c.p << 3) | (uint32_t)j;
+        const uint32_t o = (act && j < K) ? ord_of(cv[j]) : 0u;
+        k[j] = ((uint64_t)o << 32) | (~code);
     }
-    local_sort<K>(v, id);
+    local_sort<K>(k);
     const uint32_t R = C > np ? np + 1 : C;
     float prev = 0.0f;
     bool tie = false;
-    val = 0.0f;
-    src = 0;
-    jsel = 0;
+    uint64_t mine = 0;
     for (uint32_t r = 0; r < R; ++r) {
-        float bv = v[0];
-        uint32_t code = (c.p << 3) | id[0];
-        grp_max<LP>(bv, code);
-        if (r > 0 && bv == prev)
-            tie = true;
+        uint64_t h = k[0];
+        grp_kmax<LP>(h);
+        const float bv = val_of((uint32_t)(h >> 32));
+        tie = tie | ((r > 0) & (bv == prev));
         prev = bv;
-        if (r < np && c.p == r) {
-            val = bv;
-            src = code >> 3;
-            jsel = code & 7u;
-        }
-        if ((code >> 3) == c.p) { // the winner pops its head
+        mine = (r < np && c.p == r) ? h : mine;
+        const bool win = k[0] == h; // keys are unique: exactly one lane pops its head
 #pragma unroll
-            for (int j = 0; j < K - 1; ++j) {
-                v[j] = v[j + 1];
-                id[j] = id[j + 1];
-            }
-            v[K - 1] = -__builtin_inff();
-        }
+        for (int j = 0; j < K - 1; ++j)
+            k[j] = win ? k[j + 1] : k[j];
+        k[K - 1] = win ? 0ull : k[K - 1];
     }
-    if (ballot(tie) == 0ull)
+    val = val_of((uint32_t)(mine >> 32));
+    const uint32_t mc = ~(uint32_t)mine;
+    src = (mc >> 3) & 31u;
+    jsel = mc & 7u;
+    if (ballot(tie) == 0ull) {
+        LS_STAMP(c, 50);
         return;
+    }
     // literal simplePartialSortDescending per group (rare: exact metric ties)
     float* cval = c.gs + ls_gl_alpha_floats(c.mt, c.Sl) + c.gb * 8u;
     uint32_t* cid = reinterpret_cast<uint32_t*>(cval + 512);
@@ -762,6 +777,7 @@ PCG_DEV void ls_select(const Ls<LP>& c, const float (&cv)[8], uint32_t P, uint32
 template <int LP>
 PCG_DEV void ls_dup(Ls<LP>& c, uint32_t srcp, uint32_t nw, bool act)
 {
+    LS_T0();
     const int sl = (int)(c.gb | srcp);
     const uint32_t lo = shfl((uint32_t)c.ptr, sl), hi = shfl((uint32_t)(c.ptr >> 32), sl);
     c.ptr = ((uint64_t)hi << 32) | lo;
@@ -786,6 +802,7 @@ PCG_DEV void ls_dup(Ls<LP>& c, uint32_t srcp, uint32_t nw, bool act)
         if (act)
             row[w << 6] = x;
     }
+    LS_STAMP(c, 51);
 }
 
 // ---- branching leaves at n >= 8 (Rate-1 :353-413, SPC :498-621) ----------------------
@@ -797,6 +814,7 @@ PCG_DEV void ls_branch_leaf(Ls<LP>& c, Src src, uint32_t code, uint32_t s, uint3
     const uint32_t kk = code == OP_S_R1 ? 2u : 4u;
     float T[4];
     uint32_t I[4], par = 0;
+    LS_T0();
     if (n == 8) {
         const float4 a = src.ld(0, sl), b = src.ld(1, sl);
         const float v[8] = { a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w };
@@ -807,6 +825,7 @@ PCG_DEV void ls_branch_leaf(Ls<LP>& c, Src src, uint32_t code, uint32_t s, uint3
         if (tie)
             ls_weak(c, src, sl, n, kk, T, I, par);
     }
+    LS_STAMP(c, 53);
     float cv[8];
     r1_spc_cands(code, c.m, T, par, cv);
     float val;
@@ -1008,6 +1027,7 @@ PCG_DEV void st8_branch(Ls<LP>& c, LsSt8& st, uint32_t kind, const float (&v)[4]
         np = C < c.L ? C : c.L;
         ls_select<LP, 2>(c, cv, st.P, np, val, sp, j);
     }
+    LS_T0();
     const int sl = (int)(c.gb | sp);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -1022,6 +1042,7 @@ PCG_DEV void st8_branch(Ls<LP>& c, LsSt8& st, uint32_t kind, const float (&v)[4]
     c.m = val;
     st.P = np;
     st.branched = true;
+    LS_STAMP(c, 52);
 }
 
 template <int LP>
@@ -1124,6 +1145,7 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
     c.lds = smem;
 #ifdef PCG_LS_PROF
     uint64_t* lprof = reinterpret_cast<uint64_t*>(smem + a.wave_lds_floats);
+    c.lprof = lprof;
     if (threadIdx.x == 0)
         for (int b = 0; b < 64; ++b)
             lprof[b] = 0;

@@ -21,7 +21,7 @@ torch.cuda.synchronize()
 buf = (C.c_ulonglong * 128)()
 _native.lib().pcg_dev_opprof_fetch(buf)
 names = {1: "F lds", 2: "G lds", 9: "F gl->gl", 10: "G gl->gl", 17: "F virt", 18: "G virt", 25: "F gl->lds",
-         26: "G gl->lds", 4: "COMB", 40: "R0", 41: "R1", 43: "SPC", 44: "ST8", 60: "final"}
+         26: "G gl->lds", 4: "COMB", 40: "R0", 41: "R1", 43: "SPC", 44: "ST8", 60: "final", 50: "~select", 51: "~dup", 52: "~st8 move", 53: "~weak"}
 groups = buf[62]
 tot = buf[61]
 print(f"groups {groups}  cycles/group {tot / max(groups, 1):.0f}")
