@@ -1287,7 +1287,7 @@ int sclls_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* ld
     const uint32_t top = (uint32_t)__builtin_ctz(N);
     if (top > 3 + 12) // 5-bit slot fields for stages 3 .. top-1 in 64 bits
         return -4;
-    uint32_t budget = 20 * 1024 / 4; // floats per wave: occupancy beats LDS-resident stages
+    uint32_t budget = 24 * 1024 / 4; // floats per wave (measured best at N = 1024, L = 8: S_l = 6, 7 waves/CU)
     if (const char* e = getenv("PCG_SCL_LDS_KB"))
         budget = (uint32_t)atoi(e) * 1024 / 4;
     uint32_t vt = ls_max_virt(top);
