@@ -1,6 +1,7 @@
 // capi.cpp -- the C ABI of include/pcg.h on top of the HIP kernels.
 #include "../../include/pcg.h"
 
+#include "frames.hpp"
 #include "kernels.hpp"
 #include "plan.hpp"
 
@@ -29,6 +30,9 @@ struct pcg_plan {
     uint8_t* d_ok = nullptr;
     float* d_met = nullptr;
     uint64_t stage_frames = 0;
+    // pcg_decode_punctured_f32: depunctured LLRs (F x N), reused across calls
+    float* d_dep = nullptr;
+    uint64_t dep_frames = 0;
 };
 
 namespace {
@@ -72,9 +76,14 @@ void free_plan_device(pcg_plan* p)
     (void)hipFree(p->d_info);
     (void)hipFree(p->d_ok);
     (void)hipFree(p->d_met);
+    (void)hipFree(p->d_dep);
 }
 
 } // namespace
+
+namespace pcg {
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
+} // namespace pcg
 
 extern "C" {
 
@@ -318,6 +327,54 @@ int pcg_decode_f32_host(pcg_plan* p, const float* llr, uint64_t F, uint8_t* info
             (e = hipMemcpy(metrics + f0 * h.L, p->d_met, n * h.L * sizeof(float), hipMemcpyDeviceToHost)) !=
                 hipSuccess)
             return hip_fail(e, "hipMemcpy(D2H metrics)");
+    }
+    return PCG_OK;
+}
+
+int pcg_decode_punctured_f32(pcg_plan* p,
+                             const pcg_puncturer* punc,
+                             const float* llr,
+                             uint64_t F,
+                             uint8_t* info,
+                             uint8_t* ok,
+                             float* metrics,
+                             void* stream)
+{
+    if (!p || !punc)
+        return fail(PCG_E_ARG, "null plan/puncturer");
+    if (punc->N != p->host.N)
+        return fail(PCG_E_ARG, "puncturer parent length != decoder block length");
+    if (F == 0)
+        return PCG_OK;
+    if (!llr || !info)
+        return fail(PCG_E_ARG, "null llr/info buffer");
+    if (p->device < 0 || punc->device < 0)
+        return fail(PCG_E_NODEVICE, "host-only plan or puncturer");
+    if (p->device != punc->device)
+        return fail(PCG_E_ARG, "plan and puncturer live on different devices");
+    DeviceGuard g(p->device);
+    const auto& h = p->host;
+    const uint64_t kb = (h.K + 7) / 8;
+    // depunctured staging: at most 256 MB per chunk
+    const uint64_t chunk = std::min<uint64_t>(F, std::max<uint64_t>(1, (1ull << 26) / h.N));
+    if (p->dep_frames < chunk) {
+        (void)hipFree(p->d_dep);
+        p->d_dep = nullptr;
+        p->dep_frames = 0;
+        hipError_t e = hipMalloc(&p->d_dep, chunk * h.N * sizeof(float));
+        if (e != hipSuccess)
+            return hip_fail(e, "hipMalloc(depuncture staging)");
+        p->dep_frames = chunk;
+    }
+    for (uint64_t f0 = 0; f0 < F; f0 += chunk) {
+        const uint64_t n = std::min(chunk, F - f0);
+        int rc = pcg_depuncture_f32(punc, llr + f0 * punc->E, n, p->d_dep, stream);
+        if (rc != 0)
+            return rc;
+        rc = pcg_decode_f32(p, p->d_dep, n, info + f0 * kb, ok ? ok + f0 : nullptr,
+                            metrics ? metrics + f0 * h.L : nullptr, stream);
+        if (rc != 0)
+            return rc;
     }
     return PCG_OK;
 }

@@ -7,6 +7,9 @@
 //                                                        big-endian in the last 2 bytes
 //   CRC32  src/polarcode/errordetection/crc32.cpp:28-66  CRC-32C (_mm_crc32_u32) over
 //                                                        little-endian words, init 0
+//   CRC11  not in the reference: 3GPP TS 38.212 §5.1 gCRC11(D) =
+//          D^11+D^10+D^9+D^5+1, init 0, over the bit stream of the message
+//          (MSB-first bytes); the 11 parity bits occupy the last 11 bits, MSB first.
 #pragma once
 #include <cstdint>
 #include <cstring>
@@ -48,8 +51,30 @@ inline uint32_t crc32c_gen(const uint8_t* d, int words)
     return c;
 }
 
+// remainder of m(D)*D^11 mod gCRC11 over the first `nbits` bits of d (MSB-first)
+inline uint32_t crc11_gen(const uint8_t* d, int nbits)
+{
+    uint32_t c = 0;
+    for (int i = 0; i < nbits; ++i) {
+        const uint32_t fb = ((c >> 10) ^ (uint32_t)(d[i >> 3] >> (7 - (i & 7)))) & 1u;
+        c = (c << 1) & 0x7FFu;
+        if (fb)
+            c ^= 0x621u;
+    }
+    return c;
+}
+
+// the trailing 11 bits of a `bytes`-byte message
+inline uint32_t crc11_tail(const uint8_t* d, int bytes)
+{
+    uint32_t t = 0;
+    for (int i = bytes * 8 - 11; i < bytes * 8; ++i)
+        t = (t << 1) | ((uint32_t)(d[i >> 3] >> (7 - (i & 7))) & 1u);
+    return t;
+}
+
 // Syndrome of the detector over a message of `bytes` bytes: zero <=> check() passes.
-// kind: 0 (Dummy, always 0), 8, 16, 32.  Returns false for an unknown kind.
+// kind: 0 (Dummy, always 0), 8, 11, 16, 32.  Returns false for an unknown kind.
 inline bool crc_syndrome(int kind, const uint8_t* d, int bytes, uint32_t* syn)
 {
     switch (kind) {
@@ -63,6 +88,9 @@ inline bool crc_syndrome(int kind, const uint8_t* d, int bytes, uint32_t* syn)
         if (bytes < 2) { *syn = 0; return true; }
         *syn = (uint32_t)(crc16_gen(d, bytes - 2) ^
                           (uint16_t)((d[bytes - 2] << 8) | d[bytes - 1]));
+        return true;
+    case 11:
+        *syn = bytes >= 2 ? crc11_gen(d, bytes * 8 - 11) ^ crc11_tail(d, bytes) : 0u;
         return true;
     case 32: {
         int rw = (bytes >> 2) - 1;
@@ -96,6 +124,17 @@ inline bool crc_generate(int kind, uint8_t* d, int bytes)
         uint16_t c = crc16_gen(d, bytes - 2);
         d[bytes - 2] = (uint8_t)(c >> 8);
         d[bytes - 1] = (uint8_t)c;
+        return true;
+    }
+    case 11: {
+        if (bytes < 2)
+            return true;
+        const uint32_t c = crc11_gen(d, bytes * 8 - 11);
+        for (int k = 0; k < 11; ++k) {
+            const int i = bytes * 8 - 11 + k;
+            const uint8_t m = (uint8_t)(0x80u >> (i & 7));
+            d[i >> 3] = (uint8_t)(((c >> (10 - k)) & 1u) ? (d[i >> 3] | m) : (d[i >> 3] & ~m));
+        }
         return true;
     }
     case 32: {

@@ -5,6 +5,7 @@
 #include <polarcode/decoding/decoder.h>
 #include <polarcode/encoding/encoder.h>
 #include <polarcode/errordetection/errordetector.h>
+#include <polarcode/puncturer.h>
 
 #include "../crc_host.hpp"
 #include <pcg.h>
@@ -43,6 +44,8 @@ Detector* create(unsigned size, std::string type)
             return new Dummy();
         case 8:
             return new CRC8();
+        case 11:
+            return new CRC11();
         case 16:
             return new CRC16();
         case 32:
@@ -65,7 +68,7 @@ int gpuKind(Detector* d)
         return 0;
     if (t == "CRC") {
         const unsigned b = d->getCheckBitCount();
-        if (b == 0 || b == 8 || b == 16 || b == 32)
+        if (b == 0 || b == 8 || b == 11 || b == 16 || b == 32)
             return (int)b;
     }
     return -1;
@@ -76,41 +79,191 @@ int gpuKind(Detector* d)
 // =============================================================== Construction
 namespace Construction {
 
-std::vector<unsigned> frozen_bits(const int blockLength,
-                                  const int infoLength,
-                                  const float designSNR,
-                                  const std::string& constructor_type)
+namespace {
+const unsigned short kNrRank[1024] = {
+#include "nr_reliability.inc"
+};
+
+std::string lower(std::string t)
 {
-    std::string t = constructor_type;
     std::transform(t.begin(), t.end(), t.begin(), [](unsigned char c) { return std::tolower(c); });
-    if (t.find("be") != std::string::npos || t.find("5g") != std::string::npos)
-        throw std::logic_error("construction '" + constructor_type + "' is not part of this build");
-    const int N = blockLength, K = infoLength;
-    if (N < 1 || (N & (N - 1)) || K < 0 || K > N)
-        throw std::invalid_argument("block length must be a power of two and 0 <= K <= N");
-    // Bhattacharyya bounds, bhattacharrya.cpp:39-82
-    const float lin = (float)std::pow(10.0, designSNR / 10.0);
+    return t;
+}
+
+void check_lengths(size_t N, size_t K)
+{
+    if (N < K) // fiveGList.cpp:30-34, betaexpansion.cpp:47-51
+        throw std::invalid_argument("Invalid polar code(" + std::to_string(N) + ", " + std::to_string(K) + ")");
+}
+} // namespace
+
+void Constructor::setBlockLength(size_t newBlockLength)
+{
+    const size_t test = newBlockLength ? (size_t)1 << (size_t)std::log2((double)newBlockLength) : 0;
+    if (test != newBlockLength) // constructor.cpp:25-32
+        throw std::invalid_argument("new blockLength is not a power of 2!");
+    mBlockLength = newBlockLength;
+}
+
+Bhattacharrya::Bhattacharrya(size_t N, size_t K, float designSnr)
+{
+    setBlockLength(N);
+    setInformationLength(K);
+    setDesignSnr(designSnr);
+}
+
+std::vector<unsigned> Bhattacharrya::construct()
+{
+    const size_t N = mBlockLength, K = mInformationLength;
+    if (K > N)
+        throw std::invalid_argument("information length exceeds block length");
+    // initial parameter in float (bhattacharrya.cpp:39-44), recursion in double (:66-80)
+    const float lin = (float)std::pow(10.0, mDesignSnr / 10.0);
     const float init = (float)std::exp(-2.0 * lin * K / N);
     std::vector<double> z(N);
     z[0] = init;
-    for (int stage = (int)std::log2(N) - 1; stage >= 0; --stage) {
-        const int B = 1 << stage;
-        for (int j = 0; j < N; j += 2 * B) {
+    for (int stage = (int)std::log2((double)N) - 1; stage >= 0; --stage) {
+        const size_t B = (size_t)1 << stage;
+        for (size_t j = 0; j < N; j += 2 * B) {
             const double T = z[j];
             z[j + B] = T * T;
             z[j] = 2 * T - z[j + B];
         }
     }
-    std::vector<int> perm(N);
-    for (int i = 0; i < N; ++i)
-        perm[i] = i;
-    std::stable_sort(perm.begin(), perm.end(), [&](int a, int b) { return z[a] > z[b]; });
+    // trackingSorter::stableSortDescending (arrayfuncs.cpp:93-107)
+    std::vector<unsigned> perm(N);
+    for (size_t i = 0; i < N; ++i)
+        perm[i] = (unsigned)i;
+    std::stable_sort(perm.begin(), perm.end(), [&](unsigned a, unsigned b) { return z[a] > z[b]; });
     std::vector<unsigned> f(perm.begin(), perm.begin() + (N - K));
     std::sort(f.begin(), f.end());
     return f;
 }
 
+FiveGList::FiveGList(size_t N, size_t K)
+{
+    if (N > 1024) // fiveGList.cpp:21-23
+        throw std::invalid_argument("5G standard does not allow for block size N > 1024!");
+    setBlockLength(N);
+    setInformationLength(K);
+}
+
+std::vector<unsigned> FiveGList::construct()
+{
+    check_lengths(mBlockLength, mInformationLength);
+    // the first N-K entries of the 1024-entry sequence, ascending (fiveGList.cpp:35-39):
+    // exactly the indices whose reliability rank is < N-K
+    const unsigned nf = (unsigned)(mBlockLength - mInformationLength);
+    std::vector<unsigned> f;
+    f.reserve(nf);
+    for (unsigned i = 0; i < 1024; ++i)
+        if (kNrRank[i] < nf)
+            f.push_back(i);
+    return f;
+}
+
+BetaExpansion::BetaExpansion(size_t N, size_t K)
+{
+    setBlockLength(N);
+    setInformationLength(K);
+}
+
+std::vector<unsigned> BetaExpansion::construct()
+{
+    check_lengths(mBlockLength, mInformationLength);
+    const unsigned n = (unsigned)std::log2((double)mBlockLength);
+    const double beta = std::pow(2.0, 1.0 / 4.0);
+    std::vector<double> wj(n), w(mBlockLength);
+    for (unsigned j = 0; j < n; ++j)
+        wj[j] = std::pow(beta, (double)j);
+    for (size_t i = 0; i < mBlockLength; ++i) {
+        double acc = 0.0;
+        for (unsigned j = 0; j < n; ++j)
+            acc += wj[j] * ((i >> j) & 1u);
+        w[i] = acc;
+    }
+    // argsort ascending with the same std::sort call shape (betaexpansion.cpp:19-31)
+    std::vector<size_t> idx(mBlockLength);
+    for (size_t i = 0; i < mBlockLength; ++i)
+        idx[i] = i;
+    std::sort(idx.begin(), idx.end(), [&w](int l, int r) -> bool { return w[l] < w[r]; });
+    std::vector<unsigned> f(idx.begin(), idx.begin() + (mBlockLength - mInformationLength));
+    std::sort(f.begin(), f.end());
+    return f;
+}
+
+std::vector<unsigned> frozen_bits(const int blockLength,
+                                  const int infoLength,
+                                  const float designSNR,
+                                  const std::string& constructor_type)
+{
+    const std::string t = lower(constructor_type);
+    if (t.find("be") != std::string::npos)
+        return BetaExpansion((size_t)blockLength, (size_t)infoLength, designSNR).construct();
+    if (t.find("5g") != std::string::npos)
+        return FiveGList((size_t)blockLength, (size_t)infoLength, designSNR).construct();
+    return Bhattacharrya((size_t)blockLength, (size_t)infoLength, designSNR).construct();
+}
+
 } // namespace Construction
+
+// =============================================================== Puncturer
+size_t round_up_power_of_two(size_t value)
+{
+    // the 32-bit bit trick, deliberately unextended (puncturer.cpp:23-33)
+    value--;
+    value |= value >> 1;
+    value |= value >> 2;
+    value |= value >> 4;
+    value |= value >> 8;
+    value |= value >> 16;
+    return value + 1;
+}
+
+std::vector<unsigned> inverse_set_difference(size_t blockLength, std::vector<unsigned> positions)
+{
+    // the std::set_difference merge over iota(blockLength) and `positions`
+    std::vector<unsigned> out;
+    size_t j = 0;
+    for (unsigned v = 0; v < blockLength;) {
+        if (j == positions.size()) {
+            out.push_back(v++);
+        } else if (v < positions[j]) {
+            out.push_back(v++);
+        } else {
+            if (!(positions[j] < v))
+                ++v;
+            ++j;
+        }
+    }
+    return out;
+}
+
+Puncturer::Puncturer(const size_t blockLength, const std::vector<unsigned> frozenBitPositions)
+    : mBlockLength(blockLength)
+{
+    mParentBlockLength = round_up_power_of_two(mBlockLength);
+    const size_t np = mParentBlockLength - mBlockLength;
+    if (np > frozenBitPositions.size())
+        throw std::out_of_range("Number of required puncturing positions exceeds frozen bit positions!");
+    mOutputPositions = inverse_set_difference(
+        mParentBlockLength, std::vector<unsigned>(frozenBitPositions.begin(), frozenBitPositions.begin() + np));
+}
+
+Puncturer::~Puncturer() {}
+
+void Puncturer::puncturePacked(unsigned char* pOutput, const unsigned char* pInput)
+{
+    const size_t bytes = mBlockLength / 8;
+    for (size_t b = 0; b < bytes; ++b) {
+        unsigned o = 0;
+        for (unsigned i = 0; i < 8; ++i) {
+            const unsigned p = mOutputPositions[8 * b + i];
+            o |= ((pInput[p / 8] >> (7 - p % 8)) & 1u) << (7 - i);
+        }
+        pOutput[b] = (unsigned char)o;
+    }
+}
 
 // =============================================================== Encoding
 namespace Encoding {

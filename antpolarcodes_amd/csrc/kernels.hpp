@@ -14,7 +14,7 @@ struct KernelArgs {
     const uint16_t* info_pos; // K info positions (device)
     const uint32_t* crc_m;    // K syndrome columns (device)
     uint32_t crc_c0;
-    uint32_t crc_bits;        // 0, 8, 16, 32
+    uint32_t crc_bits;        // 0, 8, 11, 16, 32
     const uint32_t* crc_rows; // crc_bits x W codeword masks (device): syndrome bit r = c0_r ^ parity(cw & row r)
     int systematic;
     uint8_t* info;            // F x kb (device)

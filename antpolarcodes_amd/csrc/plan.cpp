@@ -207,7 +207,7 @@ int build_plan(PlanHost& p,
             return -1;
         }
     }
-    if (crc_kind != 0 && crc_kind != 8 && crc_kind != 16 && crc_kind != 32) {
+    if (crc_kind != 0 && crc_kind != 8 && crc_kind != 11 && crc_kind != 16 && crc_kind != 32) {
         *err = "CRC INVALID SIZE!"; // errordetector.cpp:33-35
         return -1;
     }

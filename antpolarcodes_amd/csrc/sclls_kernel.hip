@@ -1233,6 +1233,7 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
         uint32_t syn;
         switch (a.crc_bits) {
         case 8: syn = crc_syn<8>(row, a.crc_rows, W, a.crc_c0); break;
+        case 11: syn = crc_syn<11>(row, a.crc_rows, W, a.crc_c0); break;
         case 16: syn = crc_syn<16>(row, a.crc_rows, W, a.crc_c0); break;
         case 32: syn = crc_syn<32>(row, a.crc_rows, W, a.crc_c0); break;
         default: syn = a.crc_c0; break;

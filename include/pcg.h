@@ -20,6 +20,17 @@
  *   pcg_decode_f32_host <- the same with host buffers (H2D + decode + D2H)
  *   pcg_plan_destroy  <- Decoder::~Decoder decoder.cpp:104-114
  *   pcg_last_error    <- the std::exception text the reference throws
+ *   pcg_puncturer_*   <- PolarCode::Puncturer (include/polarcode/puncturer.h:33-99,
+ *                        src/polarcode/puncturer.cpp:51-89): depuncture / puncture /
+ *                        puncturePacked over F frames on the device
+ *   pcg_decode_punctured_f32 <- Puncturer::depuncture + Decoder::decode_vector, fused
+ *                        into one call (the 5G NR uplink chain)
+ *   pcg_encoder_*, pcg_encode <- Encoding::ButterflyFipPacked + Detector::generate
+ *                        (src/polarcode/encoding/butterfly_fip_packed.cpp:45-70,
+ *                        encoder.cpp:79-90), F frames on the device
+ *   pcg_random_info, pcg_bpsk_awgn_f32 <- the simulator's frame source
+ *                        (src/simulation/simulator.cpp:850-937, bpsk.cpp:54-80,
+ *                        awgn.cpp:38-43), counter-based and reproducible from a seed
  *
  * Error model: every function returns 0 on success or a negative PCG_E* code;
  * nothing throws across the ABI.  pcg_last_error() (thread-local) describes the
@@ -47,6 +58,8 @@ extern "C" {
  * (ErrorDetection::create(size, "crc"), errordetector.cpp:23-67). */
 #define PCG_CRC_NONE 0  /* Dummy: check() always true (dummy.cpp:27)                 */
 #define PCG_CRC8 8      /* CRC-8, poly 0x07 (crc8.cpp)                              */
+#define PCG_CRC11 11    /* 3GPP TS 38.212 CRC-11 over the bit stream, parity in the
+                           last 11 bits -- NOT in the reference     */
 #define PCG_CRC16 16    /* CRC-16/CCITT-FALSE, big-endian trailer (crc16.cpp)       */
 #define PCG_CRC32C 32   /* CRC-32C over little-endian words (crc32.cpp)             */
 
@@ -67,7 +80,7 @@ typedef struct pcg_plan_desc {
 /* Build a decoding plan: classify the decoder tree exactly as the reference
  * (Fast-SSC for L == 1, SCL for L >= 2), flatten it to a device schedule and
  * upload it to `device`.  `frozen` must be strictly ascending indices < N.
- * crc_kind: PCG_CRC_NONE/8/16/32.  L <= 32. */
+ * crc_kind: PCG_CRC_NONE/8/11/16/32.  L <= 32. */
 int pcg_plan_create(pcg_plan** plan,
                     uint32_t N,
                     uint32_t L,
@@ -109,6 +122,76 @@ const char* pcg_last_error(void);
 
 /* Number of HIP devices visible (0 without a GPU); never fails. */
 int pcg_device_count(void);
+
+/* ---- rate matching: Puncturer --------------------------------------------------------
+ * Puncturer(blockLength = E, frozenBitPositions): parent length N = next power of two
+ * >= E; the first N - E entries of `frozen` (as given; frozen_bits returns them
+ * ascending) are punctured; PCG_E_ARG with the reference's std::out_of_range text
+ * ("Number of required puncturing positions exceeds frozen bit positions!") when the
+ * frozen set is too small.  device < 0: host-only (positions, no device tables). */
+typedef struct pcg_puncturer pcg_puncturer;
+
+int pcg_puncturer_create(pcg_puncturer** punc,
+                         uint32_t E,
+                         const uint32_t* frozen,
+                         uint32_t n_frozen,
+                         int device);
+
+/* E, N and (if `positions` is not NULL) the E kept parent positions, ascending
+ * (Puncturer::blockLength / parentBlockLength / blockOutputPositions). */
+int pcg_puncturer_describe(const pcg_puncturer* punc, uint32_t* E, uint32_t* N, uint32_t* positions);
+
+/* Device buffers, asynchronous on `stream`:
+ *   depuncture  in F x E floats -> out F x N floats, punctured positions = +0.0f
+ *   puncture    in F x N floats -> out F x E floats
+ *   puncture_packed  in F x N/8 MSB-first bytes -> out F x E/8 (E, N multiples of 8) */
+int pcg_depuncture_f32(const pcg_puncturer* punc, const float* in, uint64_t F, float* out, void* stream);
+int pcg_puncture_f32(const pcg_puncturer* punc, const float* in, uint64_t F, float* out, void* stream);
+int pcg_puncture_packed(const pcg_puncturer* punc, const uint8_t* in, uint64_t F, uint8_t* out, void* stream);
+
+void pcg_puncturer_destroy(pcg_puncturer* punc);
+
+/* Decode F punctured frames: llr is F x E (device), depunctured on the device into the
+ * plan's staging buffer and decoded with `plan` (whose N must equal the puncturer's
+ * parent length).  Outputs as pcg_decode_f32.  Stream-ordered; the staging buffer is
+ * reused across calls on the same plan, so calls on one plan must share one stream. */
+int pcg_decode_punctured_f32(pcg_plan* plan,
+                             const pcg_puncturer* punc,
+                             const float* llr,
+                             uint64_t F,
+                             uint8_t* info,
+                             uint8_t* ok,
+                             float* metrics,
+                             void* stream);
+
+/* ---- frame source: encoder, random information, BPSK-AWGN channel ---------------------- */
+typedef struct pcg_encoder pcg_encoder;
+
+/* ButterflyFipPacked(N, frozen) + setSystematic + setErrorDetection(crc_kind). */
+int pcg_encoder_create(pcg_encoder** enc,
+                       uint32_t N,
+                       const uint32_t* frozen,
+                       uint32_t n_frozen,
+                       int systematic,
+                       int crc_kind,
+                       int device);
+
+/* info: device F x ceil(K/8) bytes; the detector's check bits are written into it in
+ * place (as encode_vector does to its caller's buffer).  code: device F x N/8 bytes,
+ * MSB-first (Encoder::getEncodedData). */
+int pcg_encode(pcg_encoder* enc, uint8_t* info, uint64_t F, uint8_t* code, void* stream);
+
+void pcg_encoder_destroy(pcg_encoder* enc);
+
+/* Uniform random information bytes (device F x ceil(K/8)), bits past K cleared:
+ * Philox4x32-10 keyed by `seed`, counter = (frame, byte block). */
+int pcg_random_info(uint8_t* info, uint64_t F, uint32_t K, uint64_t seed, void* stream);
+
+/* BPSK (bit 0 -> +1) + AWGN of standard deviation sigma + LLR = 2 y / sigma^2 over n
+ * packed code bits per frame (device code F x n/8 -> llr F x n floats, n % 8 == 0).
+ * sigma <= 0: noiseless, llr = +-1.  Noise from Philox4x32-10 keyed by `seed`. */
+int pcg_bpsk_awgn_f32(const uint8_t* code, uint64_t F, uint32_t n, float sigma, uint64_t seed, float* llr,
+                      void* stream);
 
 #ifdef __cplusplus
 }

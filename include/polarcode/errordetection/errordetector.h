@@ -53,6 +53,14 @@ class CRC8 : public Crc
 public:
     CRC8() : Crc(8) {}
 };
+/// 3GPP TS 38.212 CRC-11 (gCRC11 = D^11+D^10+D^9+D^5+1, zero init) over the message bit
+/// stream, parity in the last 11 bits.  NOT in the reference: added for the
+/// 5G NR uplink chain (config 4); ErrorDetection::create(11, "crc") returns it.
+class CRC11 : public Crc
+{
+public:
+    CRC11() : Crc(11) {}
+};
 class CRC16 : public Crc
 {
 public:
@@ -66,12 +74,12 @@ public:
 
 extern Dummy globalDummyDetector;
 
-/// ErrorDetection::create (errordetector.cpp:23-67): "crc" sizes 0/8/16/32
-/// (std::logic_error("CRC INVALID SIZE!") otherwise); "cmac" -> std::logic_error (not
+/// ErrorDetection::create (errordetector.cpp:23-67): "crc" sizes 0/8/16/32, plus 11 (CRC11,
+/// this build's extension) (std::logic_error("CRC INVALID SIZE!") otherwise); "cmac" -> std::logic_error (not
 /// in this build); anything else std::runtime_error("Unknown Error detector requested!").
 Detector* create(unsigned size, std::string type);
 
-/// pcg.h crc kind for a detector (0, 8, 16, 32); -1 if the GPU cannot evaluate it.
+/// pcg.h crc kind for a detector (0, 8, 11, 16, 32); -1 if the GPU cannot evaluate it.
 int gpuKind(Detector* d);
 
 } // namespace ErrorDetection

@@ -478,6 +478,23 @@ static uint32_t crc32c_gen(const uint8_t* d, int words)
     return c;
 }
 
+/* CRC-11 -- NOT in the reference (parity unpinned).  3GPP TS 38.212
+ * §5.1 gCRC11(D) = D^11+D^10+D^9+D^5+1, zero init, computed over the message bit
+ * stream (bytes MSB-first); the parity bits are the last 11 bits, MSB first.  Written
+ * as the textbook polynomial long division of m(D)*D^11 (a different formulation
+ * from the product's shift register, so the two check each other). */
+static uint32_t crc11_div(const uint8_t* d, int nbits)
+{
+    /* long division over a bit array: r holds 12 bits, shift in message then 11 zeros */
+    uint32_t r = 0;
+    for (int i = 0; i < nbits + 11; ++i) {
+        uint32_t b = i < nbits ? (uint32_t)((d[i / 8] >> (7 - i % 8)) & 1) : 0u;
+        r = (r << 1) | b;
+        if (r & 0x800u) r ^= 0xE21u; /* 1110 0010 0001 = D^11+D^10+D^9+D^5+1 */
+    }
+    return r & 0x7FFu;
+}
+
 /* crc: -1 -> CRC-8 (what makeDecoder installs, decoder.cpp:85), 0 -> Dummy (always ok) */
 int orc_crc(int crc, int generate, uint8_t* data, int bytes)
 {
@@ -498,6 +515,20 @@ int orc_crc(int crc, int generate, uint8_t* data, int bytes)
             return 0;
         }
         return c == (uint16_t)((data[bytes - 2] << 8) | data[bytes - 1]);
+    }
+    case 11: {
+        int nb = bytes * 8 - 11;
+        uint32_t c = crc11_div(data, nb), t = 0;
+        for (int k = 0; k < 11; ++k) {
+            int i = nb + k;
+            uint8_t m = (uint8_t)(0x80u >> (i % 8));
+            if (generate) {
+                if ((c >> (10 - k)) & 1u) data[i / 8] |= m; else data[i / 8] &= (uint8_t)~m;
+            } else {
+                t = (t << 1) | (uint32_t)((data[i / 8] & m) != 0);
+            }
+        }
+        return generate ? 0 : (int)(c == t);
     }
     case 32: {
         int rw = (bytes >> 2) - 1;
