@@ -18,7 +18,7 @@ PCG_E_HIP = -3
 PCG_E_UNSUPPORTED = -4
 PCG_E_NODEVICE = -5
 
-CRC_KINDS = (0, 8, 16, 32)
+CRC_KINDS = (0, 8, 11, 16, 32)
 
 
 class PcgError(RuntimeError):
@@ -78,6 +78,20 @@ def lib():
         L.pcg_plan_destroy.restype = None
         L.pcg_last_error.restype = C.c_char_p
         L.pcg_device_count.restype = C.c_int
+        L.pcg_puncturer_create.argtypes = [C.POINTER(P), C.c_uint32, P, C.c_uint32, C.c_int]
+        L.pcg_puncturer_describe.argtypes = [P, P, P, P]
+        L.pcg_depuncture_f32.argtypes = [P, P, C.c_uint64, P, P]
+        L.pcg_puncture_f32.argtypes = [P, P, C.c_uint64, P, P]
+        L.pcg_puncture_packed.argtypes = [P, P, C.c_uint64, P, P]
+        L.pcg_puncturer_destroy.argtypes = [P]
+        L.pcg_puncturer_destroy.restype = None
+        L.pcg_decode_punctured_f32.argtypes = [P, P, P, C.c_uint64, P, P, P, P]
+        L.pcg_encoder_create.argtypes = [C.POINTER(P), C.c_uint32, P, C.c_uint32, C.c_int, C.c_int, C.c_int]
+        L.pcg_encode.argtypes = [P, P, C.c_uint64, P, P]
+        L.pcg_encoder_destroy.argtypes = [P]
+        L.pcg_encoder_destroy.restype = None
+        L.pcg_random_info.argtypes = [P, C.c_uint64, C.c_uint32, C.c_uint64, P]
+        L.pcg_bpsk_awgn_f32.argtypes = [P, C.c_uint64, C.c_uint32, C.c_float, C.c_uint64, P, P]
         _lib = L
     return _lib
 
@@ -89,6 +103,24 @@ def _check(rc):
 
 def device_count():
     return lib().pcg_device_count()
+
+
+def _ptr(t):
+    if t is None:
+        return None
+    return t if isinstance(t, int) else t.data_ptr()
+
+
+def _stream(stream, t):
+    if stream is not None:
+        return stream
+    import torch
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _frozen_array(frozen):
+    fr = np.ascontiguousarray(np.asarray(list(frozen), dtype=np.uint32))
+    return fr, (fr.ctypes.data if fr.size else None)
 
 
 class Plan:
@@ -132,6 +164,11 @@ class Plan:
             stream = torch.cuda.current_stream(llr.device).cuda_stream
         _check(lib().pcg_decode_f32(self._h, ptr(llr), F, ptr(info), ptr(ok), ptr(metrics), stream))
 
+    def decode_punctured_device(self, punc, llr, info, ok=None, metrics=None, stream=None):
+        """Depuncture (F x E, device) with `punc` and decode, one stream-ordered call."""
+        _check(lib().pcg_decode_punctured_f32(self._h, punc._h, _ptr(llr), llr.shape[0], _ptr(info), _ptr(ok),
+                                              _ptr(metrics), _stream(stream, llr)))
+
     def close(self):
         if getattr(self, "_h", None):
             lib().pcg_plan_destroy(self._h)
@@ -142,3 +179,79 @@ class Plan:
             self.close()
         except Exception:
             pass
+
+
+class Puncturer:
+    """pcg_puncturer: Puncturer(E, frozen) (puncturer.cpp:51-66) with device tables."""
+
+    def __init__(self, E, frozen, device=0):
+        fr, fp = _frozen_array(frozen)
+        h = C.c_void_p()
+        _check(lib().pcg_puncturer_create(C.byref(h), int(E), fp, int(fr.size), int(device)))
+        self._h = h
+        e, n = C.c_uint32(), C.c_uint32()
+        _check(lib().pcg_puncturer_describe(h, C.byref(e), C.byref(n), None))
+        self.E, self.N, self.device = e.value, n.value, device
+
+    def positions(self):
+        out = np.zeros(self.E, np.uint32)
+        _check(lib().pcg_puncturer_describe(self._h, None, None, out.ctypes.data))
+        return out
+
+    def depuncture_device(self, x, out, stream=None):
+        _check(lib().pcg_depuncture_f32(self._h, _ptr(x), x.shape[0], _ptr(out), _stream(stream, x)))
+
+    def puncture_device(self, x, out, stream=None):
+        _check(lib().pcg_puncture_f32(self._h, _ptr(x), x.shape[0], _ptr(out), _stream(stream, x)))
+
+    def puncture_packed_device(self, x, out, stream=None):
+        _check(lib().pcg_puncture_packed(self._h, _ptr(x), x.shape[0], _ptr(out), _stream(stream, x)))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().pcg_puncturer_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Encoder:
+    """pcg_encoder: ButterflyFipPacked + Detector::generate on the device."""
+
+    def __init__(self, N, frozen, systematic=True, crc=0, device=0):
+        fr, fp = _frozen_array(frozen)
+        h = C.c_void_p()
+        _check(lib().pcg_encoder_create(C.byref(h), int(N), fp, int(fr.size), int(bool(systematic)), int(crc),
+                                        int(device)))
+        self._h = h
+        self.N, self.K = int(N), int(N) - int(fr.size)
+        self.kb = (self.K + 7) // 8
+        self.device = device
+
+    def encode_device(self, info, code, stream=None):
+        """info (F x kb uint8, check bits written in place) -> code (F x N/8 uint8)."""
+        _check(lib().pcg_encode(self._h, _ptr(info), info.shape[0], _ptr(code), _stream(stream, info)))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().pcg_encoder_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def random_info_device(info, K, seed, stream=None):
+    _check(lib().pcg_random_info(_ptr(info), info.shape[0], int(K), int(seed) & (2**64 - 1), _stream(stream, info)))
+
+
+def bpsk_awgn_device(code, n, sigma, seed, llr, stream=None):
+    _check(lib().pcg_bpsk_awgn_f32(_ptr(code), code.shape[0], int(n), float(sigma), int(seed) & (2**64 - 1),
+                                   _ptr(llr), _stream(stream, code)))

@@ -1,6 +1,6 @@
 // pypolar_bindings.cpp -- pybind11 module `_pypolar` with the reference's `pypolar`
 // surface (python/bindings/*.cc of david13pod/antPolarCodes): PolarDecoder,
-// PolarEncoder, Detector, frozen_bits -- same names, arguments and error messages --
+// PolarEncoder, Detector, Puncturer, frozen_bits -- same names, arguments and error messages --
 // plus PolarDecoder.decode_batch / decode_device for batched GPU decoding.
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
@@ -10,6 +10,7 @@
 #include <polarcode/decoding/decoder.h>
 #include <polarcode/encoding/encoder.h>
 #include <polarcode/errordetection/errordetector.h>
+#include <polarcode/puncturer.h>
 
 #include <cstring>
 #include <memory>
@@ -33,6 +34,36 @@ struct PyEncoder {
 
 using f32array = py::array_t<float, py::array::c_style | py::array::forcecast>;
 using u8array = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
+using f64array = py::array_t<double, py::array::c_style | py::array::forcecast>;
+
+// Puncturer.puncture / depuncture for one element type (puncturer_python.cc:37-160)
+template <typename T>
+py::array_t<T> do_puncture(Puncturer& self, const py::array_t<T, py::array::c_style | py::array::forcecast>& a)
+{
+    py::buffer_info in = a.request();
+    if (in.ndim != 1)
+        throw std::runtime_error("Only ONE-dimensional vectors allowed!");
+    if ((size_t)in.size != self.parentBlockLength())
+        throw std::runtime_error("Input vector size != parentBlockSize!");
+    auto res = py::array_t<T>(self.blockLength());
+    self.puncture<T>(res.mutable_data(), static_cast<const T*>(in.ptr));
+    return res;
+}
+
+template <typename T>
+py::array_t<T> do_depuncture(Puncturer& self,
+                             const py::array_t<T, py::array::c_style | py::array::forcecast>& a,
+                             const char* sizeMsg)
+{
+    py::buffer_info in = a.request();
+    if (in.ndim != 1)
+        throw std::runtime_error("Only ONE-dimensional vectors allowed!");
+    if ((size_t)in.size != self.blockLength())
+        throw std::runtime_error(sizeMsg);
+    auto res = py::array_t<T>(self.parentBlockLength());
+    self.depuncture<T>(res.mutable_data(), static_cast<const T*>(in.ptr));
+    return res;
+}
 
 } // namespace
 
@@ -159,7 +190,10 @@ PYBIND11_MODULE(_pypolar, m)
                  py::buffer_info in = a.request();
                  if (in.ndim != 1)
                      throw std::runtime_error("Only ONE-dimensional vectors allowed!");
-                 auto res = py::array_t<uint8_t>(in.size + self.getCheckBitCount() / 8);
+                 // byte-sized checksums are appended (detector_python.cc); CRC-11 (this
+                 // build's extension) writes its 11 bits over the tail of the given bytes
+                 const unsigned cb = self.getCheckBitCount();
+                 auto res = py::array_t<uint8_t>(in.size + (cb % 8 ? 0 : cb / 8));
                  py::buffer_info rb = res.request();
                  std::memcpy(rb.ptr, in.ptr, in.size);
                  self.generate(rb.ptr, (int)rb.size);
@@ -171,6 +205,34 @@ PYBIND11_MODULE(_pypolar, m)
                 throw std::runtime_error("Only ONE-dimensional vectors allowed!");
             std::vector<uint8_t> tmp(static_cast<uint8_t*>(in.ptr), static_cast<uint8_t*>(in.ptr) + in.size);
             return self.check(tmp.data(), (int)tmp.size());
+        });
+
+    // overload order as the reference registers them: double, float, uint8
+    py::class_<Puncturer>(m, "Puncturer")
+        .def(py::init<size_t, std::vector<unsigned>>(), py::arg("blockLength"), py::arg("frozenBitPositions"))
+        .def("blockLength", &Puncturer::blockLength)
+        .def("parentBlockLength", &Puncturer::parentBlockLength)
+        .def("blockOutputPositions", &Puncturer::blockOutputPositions)
+        .def("puncturePacked",
+             [](Puncturer& self, const u8array& a) {
+                 py::buffer_info in = a.request();
+                 if (in.ndim != 1)
+                     throw std::runtime_error("Only ONE-dimensional vectors allowed!");
+                 if ((size_t)in.size != self.parentBlockLength() / 8)
+                     throw std::runtime_error("Input vector size != parentBlockSize!");
+                 auto res = py::array_t<uint8_t>(self.blockLength() / 8);
+                 self.puncturePacked(res.mutable_data(), static_cast<const uint8_t*>(in.ptr));
+                 return res;
+             })
+        .def("puncture", [](Puncturer& s, const f64array& a) { return do_puncture<double>(s, a); })
+        .def("puncture", [](Puncturer& s, const f32array& a) { return do_puncture<float>(s, a); })
+        .def("puncture", [](Puncturer& s, const u8array& a) { return do_puncture<uint8_t>(s, a); })
+        .def("depuncture",
+             [](Puncturer& s, const f64array& a) { return do_depuncture<double>(s, a, "Input vector size != blockSize!"); })
+        .def("depuncture",
+             [](Puncturer& s, const f32array& a) { return do_depuncture<float>(s, a, "Input vector size != blockSize!"); })
+        .def("depuncture", [](Puncturer& s, const u8array& a) {
+            return do_depuncture<uint8_t>(s, a, "Input vector size != bBlockSize!");
         });
 
     m.def("frozen_bits", &Construction::frozen_bits, py::arg("blockLength"), py::arg("infoLength"),

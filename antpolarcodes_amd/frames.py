@@ -63,6 +63,17 @@ def crc_generate(kind, data):
             c = (t[((c >> 8) ^ d[:, i]) & 0xFF] ^ (c << 8)).astype(np.uint16)
         d[:, B - 2] = (c >> 8).astype(np.uint8)
         d[:, B - 1] = (c & 0xFF).astype(np.uint8)
+    elif kind == 11:
+        # 3GPP TS 38.212 gCRC11 over the bit stream, parity in the last 11 bits
+        bits = np.unpackbits(d, axis=1)
+        nb = B * 8 - 11
+        c = np.zeros(F, np.uint32)
+        for i in range(nb):
+            fb = ((c >> 10) ^ bits[:, i]) & 1
+            c = ((c << 1) & 0x7FF) ^ (fb * 0x621).astype(np.uint32)
+        for k in range(11):
+            bits[:, nb + k] = (c >> (10 - k)) & 1
+        d = np.packbits(bits, axis=1)
     elif kind == 32:
         t = _crc32c_table()
         rw = B // 4 - 1
@@ -122,3 +133,30 @@ def awgn_frames(N, frozen, F, ebn0_db=2.0, seed=0, crc=8, systematic=True):
     y = (1.0 - 2.0 * x.astype(np.float32)) + sigma * rng.standard_normal((F, N)).astype(np.float32)
     llr = (2.0 / (sigma * sigma) * y).astype(np.float32)
     return llr, info, x
+
+
+def nr_frames(E, K, F, ebn0_db=2.0, seed=0, crc=11, N=1024):
+    """5G NR uplink-style frames (SURVEY config 4): FiveGList(N, K) frozen set, CRC-11
+    over the K info bits (K - 11 payload bits), systematic encode, puncture to E
+    (Puncturer(E, frozen): the first N - E frozen positions), BPSK-AWGN at
+    Es/N0 = Eb/N0 * K/E.  Returns (llr F x E float32, info F x K/8 uint8, frozen, positions)."""
+    from .construction import frozen_bits
+    frozen = frozen_bits(N, K, 0.0, "5G")
+    nf = len(frozen)
+    np_ = N - E
+    if np_ > nf:
+        raise ValueError("Number of required puncturing positions exceeds frozen bit positions!")
+    pos = np.setdiff1d(np.arange(N), np.asarray(frozen[:np_], np.int64))
+    kb = (K + 7) // 8
+    rng = np.random.default_rng(seed)
+    info = rng.integers(0, 256, size=(F, kb), dtype=np.uint8)
+    if K % 8:
+        info[:, -1] &= np.uint8((0xFF << (8 - K % 8)) & 0xFF)
+    if crc:
+        info = crc_generate(crc, info)
+    x = encode(N, frozen, info, systematic=True, crc=0)[:, pos]
+    esn0 = 10.0 ** (ebn0_db / 10.0) * K / E
+    sigma = 1.0 / np.sqrt(2.0 * esn0)
+    y = (1.0 - 2.0 * x.astype(np.float32)) + sigma * rng.standard_normal((F, E)).astype(np.float32)
+    llr = (2.0 / (sigma * sigma) * y).astype(np.float32)
+    return llr, info, frozen, pos

@@ -1,6 +1,6 @@
 """Drop-in for the reference's `pypolar` module (python/__init__.py +
 python/bindings/*.cc of david13pod/antPolarCodes): PolarDecoder, PolarEncoder,
-Detector and frozen_bits with the same names, arguments and errors.
+Detector, Puncturer and frozen_bits with the same names, arguments and errors.
 
     from antpolarcodes_amd import pypolar
     dec = pypolar.PolarDecoder(1024, 8, pypolar.frozen_bits(1024, 512, 0.0), "gpu")
@@ -15,6 +15,6 @@ from ._native import _prefer_torch_hip_runtime
 
 _prefer_torch_hip_runtime()  # share PyTorch's HIP runtime (see _native.py)
 
-from ._pypolar import Detector, PolarDecoder, PolarEncoder, frozen_bits  # noqa: E402
+from ._pypolar import Detector, PolarDecoder, PolarEncoder, Puncturer, frozen_bits  # noqa: E402
 
-__all__ = ["PolarDecoder", "PolarEncoder", "Detector", "frozen_bits"]
+__all__ = ["PolarDecoder", "PolarEncoder", "Detector", "Puncturer", "frozen_bits"]

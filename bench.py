@@ -25,7 +25,10 @@ MODES = {
     "scl8": (1024, 512, 8, 1 << 16, "config 3: CRC-aided SCL L=8, N=1024 K=512, 2^16 AWGN frames"),
     "sc": (1024, 512, 1, 1 << 16, "config 2: batched Fast-SSC, N=1024 K=512, 2^16 AWGN frames"),
     "scl32": (4096, 2048, 32, 1 << 14, "config 5 shard shape: SCL L=32, N=4096 K=2048, 2^14 frames/GPU"),
+    "nr5g": (1024, 512, 8, 1 << 16, "config 4: 5G NR uplink, FiveGList N=1024 K=512 (501 + CRC-11), "
+                                     "punctured to E=896, device depuncture + SCL L=8, 2^16 frames"),
 }
+NR_E = 896
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured float4 copy)
 
 
@@ -43,7 +46,9 @@ def parse():
 
 def cpu_baseline(mode, N, L, frozen, llr, threads):
     """Reference AVX2 decoder (oracle/_ref, compiled from the reference sources) timed on
-    this host; falls back to the C restatement (oracle/liboracle.so) if absent."""
+    this host; falls back to the C restatement (oracle/liboracle.so) if absent.  For
+    nr5g the LLRs are the depunctured frames and the reference keeps the CRC-8 its
+    makeDecoder installs (it has no CRC-11)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     try:
         from pyoracle import Reference
@@ -86,9 +91,17 @@ def main():
     from antpolarcodes_amd._native import Plan
     from antpolarcodes_amd.construction import frozen_bits
 
-    frozen = frozen_bits(N, K, 0.0, "BB")
-    llr, info, _ = frames.awgn_frames(N, frozen, F, args.ebn0, seed=1000 + rank, crc=8)
-    plan = Plan(N, L, frozen, systematic=True, crc=8, device=local)
+    crc = 8
+    punc = None
+    if args.mode == "nr5g":
+        from antpolarcodes_amd._native import Puncturer
+        crc = 11
+        llr, info, frozen, pos = frames.nr_frames(NR_E, K, F, args.ebn0, seed=1000 + rank, crc=crc)
+        punc = Puncturer(NR_E, frozen, device=local)
+    else:
+        frozen = frozen_bits(N, K, 0.0, "BB")
+        llr, info, _ = frames.awgn_frames(N, frozen, F, args.ebn0, seed=1000 + rank, crc=crc)
+    plan = Plan(N, L, frozen, systematic=True, crc=crc, device=local)
     kb = plan.kb
     d_llr = torch.from_numpy(llr).to(f"cuda:{local}")
     d_info = torch.empty((F, kb), dtype=torch.uint8, device=f"cuda:{local}")
@@ -97,7 +110,10 @@ def main():
     stream = torch.cuda.current_stream()
 
     def step():
-        plan.decode_device(d_llr, d_info, d_ok, d_met, stream=stream.cuda_stream)
+        if punc is not None:
+            plan.decode_punctured_device(punc, d_llr, d_info, d_ok, d_met, stream=stream.cuda_stream)
+        else:
+            plan.decode_device(d_llr, d_info, d_ok, d_met, stream=stream.cuda_stream)
 
     for _ in range(args.warmup):
         step()
@@ -133,7 +149,8 @@ def main():
     value = total_frames / wall_max
 
     if rank == 0:
-        bytes_per_cw = 4 * N + kb + 1  # LLRs in, info bytes + ok flag out (+ metrics below)
+        # LLRs in (E per frame for nr5g), info bytes + ok flag out (+ metrics below)
+        bytes_per_cw = 4 * (NR_E if punc is not None else N) + kb + 1
         if L > 1:
             bytes_per_cw += 4 * L
         achieved = F * bytes_per_cw / (kern_ms * 1e-3) / 1e9
@@ -159,9 +176,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic BPSK-AWGN frames (Eb/N0 %.1f dB), BB(0 dB) frozen set, CRC-8" % args.ebn0,
+            "data": ("synthetic BPSK-AWGN frames (Eb/N0 %.1f dB), " % args.ebn0)
+            + ("5G reliability-list frozen set, CRC-11, punctured to E=%d" % NR_E if punc is not None
+               else "BB(0 dB) frozen set, CRC-8"),
             "config": {"workload": workload, "N": N, "K": K, "L": L, "frames_per_step_per_gpu": F,
-                       "crc": "CRC-8", "systematic": True, "parallelism": f"{world} independent shards"},
+                       "crc": "CRC-11" if crc == 11 else "CRC-8", "systematic": True,
+                       "parallelism": f"{world} independent shards"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel_ms": kern_ms, "algorithmic_bytes_per_codeword": bytes_per_cw},
@@ -169,7 +189,11 @@ def main():
             "crc_ok_rate": ok_rate,
         }
         if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(args.mode, N, L, frozen, llr, args.cpu_threads)
+            cpu_llr = llr
+            if punc is not None:
+                cpu_llr = np.zeros((llr.shape[0], N), np.float32)
+                cpu_llr[:, pos] = llr
+            line["cpu_baseline"] = cpu_baseline(args.mode, N, L, frozen, cpu_llr, args.cpu_threads)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -1118,3 +1118,47 @@ void orc_combine_short(const float* l, const float* r, float* out, uint32_t h)
         out[h + i] = r[i];
     }
 }
+
+/* ------------------------------------------------------------------ */
+/* Puncturer  src/polarcode/puncturer.cpp:23-89, include/polarcode/puncturer.h:60-99 */
+/* ------------------------------------------------------------------ */
+/* Kept parent positions for Puncturer(E, frozen): parent = next power of two >= E,
+ * the first parent-E entries of `frozen` (as given) removed from [0, parent).
+ * Returns the number of kept positions, -1 if the frozen set is too small. */
+int orc_puncturer(uint32_t E, const uint32_t* frozen, uint32_t nf, uint32_t* parent, uint32_t* pos)
+{
+    uint32_t N = 1;
+    while (N < E) N <<= 1;                 /* round_up_power_of_two, E >= 1 */
+    uint32_t np = N - E, k = 0;
+    if (np > nf) return -1;                /* std::out_of_range, puncturer.cpp:57-60 */
+    /* std::set_difference over ascending ranges (written as a membership test) */
+    for (uint32_t x = 0; x < N; ++x) {
+        int gone = 0;
+        for (uint32_t j = 0; j < np; ++j) if (frozen[j] == x) { gone = 1; break; }
+        if (!gone) pos[k++] = x;
+    }
+    *parent = N;
+    return (int)k;
+}
+
+/* depuncture (puncturer.h:92-99): zero-fill, then scatter; F frames */
+void orc_depuncture(uint32_t E, uint32_t N, const uint32_t* pos, const float* in, uint64_t F, float* out)
+{
+    for (uint64_t f = 0; f < F; ++f) {
+        for (uint32_t i = 0; i < N; ++i) out[f * N + i] = 0.0f;
+        for (uint32_t k = 0; k < E; ++k) out[f * N + pos[k]] = in[f * E + k];
+    }
+}
+
+/* puncturePacked (puncturer.cpp:71-89): MSB-first bits, one frame */
+void orc_puncture_packed(uint32_t E, const uint32_t* pos, const uint8_t* in, uint8_t* out)
+{
+    for (uint32_t b = 0; b < E / 8; ++b) {
+        uint8_t o = 0;
+        for (uint32_t i = 0; i < 8; ++i) {
+            uint32_t p = pos[8 * b + i];
+            if ((in[p / 8] >> (7 - p % 8)) & 1) o |= (uint8_t)(0x80u >> i);
+        }
+        out[b] = o;
+    }
+}

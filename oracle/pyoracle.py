@@ -48,6 +48,11 @@ class Oracle:
         lib.orc_f.argtypes = [_P, _P, _U32]
         lib.orc_g.argtypes = [_P, _P, _P, _U32]
         lib.orc_combine_short.argtypes = [_P, _P, _P, _U32]
+        lib.orc_puncturer.argtypes = [_U32, _P, _U32, _P, _P]
+        lib.orc_depuncture.argtypes = [_U32, _U32, _P, _P, _U64, _P]
+        lib.orc_depuncture.restype = None
+        lib.orc_puncture_packed.argtypes = [_U32, _P, _P, _P]
+        lib.orc_puncture_packed.restype = None
         self.lib = lib
 
     def f(self, left, right):
@@ -124,6 +129,30 @@ class Oracle:
             raise ValueError(f"invalid frozen set for Fast-SSC ({k})")
         return t[:k], s[:k]
 
+    def puncturer(self, E, frozen):
+        """(parent N, kept positions) of Puncturer(E, frozen)."""
+        fr = _frozen(frozen)
+        pos = np.zeros(2 * E + 8, np.uint32)
+        n = np.zeros(1, np.uint32)
+        r = self.lib.orc_puncturer(E, _p(fr), len(fr), _p(n), _p(pos))
+        if r < 0:
+            raise ValueError("Number of required puncturing positions exceeds frozen bit positions!")
+        return int(n[0]), pos[:r].copy()
+
+    def depuncture(self, E, frozen, x):
+        N, pos = self.puncturer(E, frozen)
+        x = np.ascontiguousarray(x, np.float32).reshape(-1, E)
+        out = np.zeros((x.shape[0], N), np.float32)
+        self.lib.orc_depuncture(E, N, _p(pos), _p(x), x.shape[0], _p(out))
+        return out
+
+    def puncture_packed(self, E, frozen, x):
+        _, pos = self.puncturer(E, frozen)
+        x = np.ascontiguousarray(x, np.uint8)
+        out = np.zeros(E // 8, np.uint8)
+        self.lib.orc_puncture_packed(E, _p(pos), _p(x), _p(out))
+        return out
+
     def frozen_bits_bb(self, N, K, dsnr):
         out = np.zeros(N, np.uint32)
         n = self.lib.orc_frozen_bits_bb(N, K, dsnr, _p(out))
@@ -150,6 +179,8 @@ class Reference:
         lib.ref_bench.argtypes = [_U32, _U32, _P, _U32, _I, _I, _P, _U64, _I, _I]
         lib.ref_bench.restype = C.c_double
         lib.ref_last_error.restype = C.c_char_p
+        lib.ref_puncturer.argtypes = [_U32, _P, _U32, _P, _P]
+        lib.ref_punc_apply.argtypes = [_U32, _P, _U32, _I, _P, _P]
         self.lib = lib
 
     @staticmethod
@@ -215,6 +246,31 @@ class Reference:
         d = np.array(data, dtype=np.uint8).copy()
         r = self.lib.ref_crc(kind, int(generate), _p(d), len(d))
         return d if generate else bool(r > 0)
+
+    def puncturer(self, E, frozen):
+        """Puncturer(E, frozen): (parent N, kept positions)."""
+        fr = _frozen(frozen)
+        pos = np.zeros(2 * E + 8, np.uint32)
+        n = np.zeros(1, np.uint32)
+        r = self.lib.ref_puncturer(E, _p(fr), len(fr), _p(n), _p(pos))
+        if r < 0:
+            raise ValueError(self.lib.ref_last_error().decode())
+        return int(n[0]), pos[:r].copy()
+
+    def punc_apply(self, E, frozen, op, x):
+        """op 0 depuncture (E floats -> N), 1 puncture (N floats -> E), 2 puncturePacked."""
+        fr = _frozen(frozen)
+        N, _ = self.puncturer(E, frozen)
+        if op == 2:
+            x = np.ascontiguousarray(x, np.uint8)
+            out = np.zeros(E // 8, np.uint8)
+        else:
+            x = np.ascontiguousarray(x, np.float32)
+            out = np.zeros(N if op == 0 else E, np.float32)
+        r = self.lib.ref_punc_apply(E, _p(fr), len(fr), op, _p(x), _p(out))
+        if r < 0:
+            raise ValueError(self.lib.ref_last_error().decode())
+        return out
 
     def bench(self, N, L, frozen, llr, threads=1, reps=1, systematic=True, crc=-1):
         fr = _frozen(frozen)

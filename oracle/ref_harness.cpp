@@ -17,12 +17,14 @@
 //   Construction::frozen_bits        src/polarcode/construction/constructor.cpp:41-63
 //   Encoding::ButterflyFipPacked     src/polarcode/encoding/butterfly_fip_packed.cpp:45-70
 //   SclAvx::PathList / createDecoder src/polarcode/decoding/scl_avx_float.cpp:21-171,624-651
+//   Puncturer                        src/polarcode/puncturer.cpp:51-89, puncturer.h:60-99
 
 #include <polarcode/construction/constructor.h>
 #include <polarcode/decoding/decoder.h>
 #include <polarcode/decoding/scl_avx_float.h>
 #include <polarcode/encoding/butterfly_fip_packed.h>
 #include <polarcode/errordetection/errordetector.h>
+#include <polarcode/puncturer.h>
 
 #include <atomic>
 #include <chrono>
@@ -63,6 +65,41 @@ Decoding::Decoder* make_dec(uint32_t N,
 extern "C" {
 
 const char* ref_last_error() { return g_err.c_str(); }
+
+// Puncturer(E, frozen): parent length into *N, the kept positions into pos (E entries);
+// returns E or -1 (std::out_of_range text in ref_last_error).
+int ref_puncturer(uint32_t E, const uint32_t* frozen, uint32_t nf, uint32_t* N, uint32_t* pos)
+{
+    try {
+        Puncturer p(E, to_vec(frozen, nf));
+        *N = (uint32_t)p.parentBlockLength();
+        auto v = p.blockOutputPositions();
+        for (size_t i = 0; i < v.size(); ++i)
+            pos[i] = v[i];
+        return (int)v.size();
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
+
+// Puncturer::depuncture<float> / puncture<float> / puncturePacked on one frame.
+int ref_punc_apply(uint32_t E, const uint32_t* frozen, uint32_t nf, int op, const void* in, void* out)
+{
+    try {
+        Puncturer p(E, to_vec(frozen, nf));
+        if (op == 0)
+            p.depuncture<float>(static_cast<float*>(out), static_cast<const float*>(in));
+        else if (op == 1)
+            p.puncture<float>(static_cast<float*>(out), static_cast<const float*>(in));
+        else
+            p.puncturePacked(static_cast<unsigned char*>(out), static_cast<const unsigned char*>(in));
+        return 0;
+    } catch (std::exception& e) {
+        g_err = e.what();
+        return -1;
+    }
+}
 
 int ref_frozen_bits(uint32_t N, uint32_t K, float dsnr, const char* type, uint32_t* out)
 {

@@ -1,0 +1,166 @@
+"""GPU parity of the rate-matching and frame-source rows and of the
+5G NR config-4 chain: device depuncture / puncture / puncturePacked against the reference
+fixtures and the oracle, the batched depuncture+decode call (CRC-11 SCL-8 and Fast-SSC)
+against the oracle on the same depunctured LLRs, the device encoder against the oracle's
+encoder for every detector, and the channel / info generators' documented properties.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+FX = np.load(os.path.join(HERE, "golden", "nr_fixtures.npz"))
+
+
+def _t(x):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(x)).to("cuda:0")
+
+
+def _cases():
+    for i in range(int(FX["punc_cases"])):
+        g = lambda k: FX[f"punc{i}_{k}"]  # noqa: E731
+        yield (int(g("E")), int(g("N")), g("frozen").astype(int).tolist(), g("x"), g("dep"), g("y"), g("pun"),
+               g("b"), g("pp"))
+
+
+def test_device_puncturer_matches_reference_fixtures():
+    import torch
+    from antpolarcodes_amd._native import Puncturer
+    for E, N, fr, x, dep, y, pun, b, pp in _cases():
+        p = Puncturer(E, fr, device=0)
+        assert (p.E, p.N) == (E, N)
+        if N % 4 == 0:
+            out = torch.full((1, N), 7.0, device="cuda:0")
+            p.depuncture_device(_t(x[None]), out)
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy()[0].view(np.uint32), dep.view(np.uint32))
+        out = torch.empty((1, E), device="cuda:0")
+        p.puncture_device(_t(y[None]), out)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy()[0], pun)
+        if b.size:
+            ob = torch.empty((1, E // 8), dtype=torch.uint8, device="cuda:0")
+            p.puncture_packed_device(_t(b[None]), ob)
+            torch.cuda.synchronize()
+            assert np.array_equal(ob.cpu().numpy()[0], pp)
+
+
+def test_device_depuncture_batch_matches_oracle(oracle):
+    import torch
+    from antpolarcodes_amd import frames
+    from antpolarcodes_amd._native import Puncturer
+    llr, _, fr, _ = frames.nr_frames(896, 512, 4099, 1.0, seed=3)
+    llr[5, :7] = -0.0
+    p = Puncturer(896, fr, device=0)
+    out = torch.empty((llr.shape[0], 1024), device="cuda:0")
+    p.depuncture_device(_t(llr), out)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), oracle.depuncture(896, fr, llr).view(np.uint32))
+
+
+@pytest.mark.parametrize("L", [1, 8])
+def test_decode_punctured_matches_oracle(oracle, L):
+    """Config 4: FiveGList(1024, 512), CRC-11, E = 896 -> depuncture + decode on the GPU."""
+    import torch
+    from antpolarcodes_amd import frames
+    from antpolarcodes_amd._native import Plan, Puncturer
+    F = 2048 if L > 1 else 8192
+    llr, info_tx, fr, _ = frames.nr_frames(896, 512, F, 1.25, seed=40 + L)
+    plan = Plan(1024, L, fr, systematic=True, crc=11, device=0)
+    punc = Puncturer(896, fr, device=0)
+    d_info = torch.empty((F, 64), dtype=torch.uint8, device="cuda:0")
+    d_ok = torch.empty(F, dtype=torch.uint8, device="cuda:0")
+    d_met = torch.empty((F, L), dtype=torch.float32, device="cuda:0") if L > 1 else None
+    plan.decode_punctured_device(punc, _t(llr), d_info, d_ok, d_met)
+    torch.cuda.synchronize()
+    dep = oracle.depuncture(896, fr, llr)
+    if L == 1:
+        oi, ook = oracle.sc_decode(1024, fr, dep, crc=11)
+    else:
+        oi, ook, om, _, _ = oracle.scl_decode(1024, L, fr, dep, crc=11, paths=True)
+        assert np.array_equal(d_met.cpu().numpy().view(np.uint32), om.view(np.uint32))
+    gi = d_info.cpu().numpy()
+    bad = np.nonzero(~(gi == oi).all(axis=1))[0]
+    assert bad.size == 0, f"frames {bad[:8]} differ"
+    assert np.array_equal(d_ok.cpu().numpy(), ook)
+    # the channel was good enough that most frames decode (sanity, not parity)
+    assert (gi == info_tx).all(axis=1).mean() > 0.5
+
+
+def test_nr_fixture_core_on_gpu():
+    """Reference-generated: SCL-8 with the Dummy detector on depunctured frames."""
+    from antpolarcodes_amd._native import Plan
+    fr = FX["nr_frozen"].astype(int).tolist()
+    p = Plan(1024, 8, fr, crc=0, device=0)
+    gi, _, gm = p.decode_host(FX["nr_llr"], want_metrics=True)
+    assert np.array_equal(gi, FX["nr_scl8_info"])
+    assert np.array_equal(gm.view(np.uint32), FX["nr_scl8_met"].view(np.uint32))
+    p1 = Plan(1024, 1, fr, crc=0, device=0)
+    gi, _, _ = p1.decode_host(FX["nr_llr"])
+    assert np.array_equal(gi, FX["nr_sc_info"])
+
+
+@pytest.mark.parametrize("crc", [0, 8, 11, 16, 32])
+@pytest.mark.parametrize("systematic", [True, False])
+def test_device_encoder_matches_oracle(oracle, crc, systematic):
+    import torch
+    from antpolarcodes_amd._native import Encoder
+    rng = np.random.default_rng(crc * 2 + systematic)
+    from antpolarcodes_amd.construction import frozen_bits
+    for N, K, kind in ((64, 32, "BB"), (1024, 512, "BB"), (1024, 512, "5G"), (1024, 700, "5G"), (2048, 1024, "BB"),
+                       (4096, 2048, "BB"), (8192, 4096, "BB"), (32, 16, "BB"), (16, 8, "BB"), (8, 8, "BB"),
+                       (512, 260, "BB")):
+        fr = frozen_bits(N, K, 0.0, kind)
+        if crc and (K // 8) * 8 < max(crc, 8) + 8:
+            continue
+        F = 67
+        info = rng.integers(0, 256, (F, (K + 7) // 8), dtype=np.uint8)
+        exp_code = oracle.encode(N, fr, info, systematic=systematic, crc=crc)
+        exp_info = info.copy()
+        if crc:
+            for r in exp_info:
+                r[:K // 8] = oracle.crc(crc, r[:K // 8], generate=True)
+        d_info = _t(info)
+        d_code = torch.empty((F, N // 8), dtype=torch.uint8, device="cuda:0")
+        Encoder(N, fr, systematic=systematic, crc=crc, device=0).encode_device(d_info, d_code)
+        torch.cuda.synchronize()
+        assert np.array_equal(d_code.cpu().numpy(), exp_code), (N, K, kind)
+        assert np.array_equal(d_info.cpu().numpy(), exp_info), (N, K, kind)
+
+
+def test_device_frame_source_round_trip(oracle):
+    """random info -> encode (CRC-8) -> noiseless BPSK -> decode == the info; with noise
+    the LLR statistics match N(2/sigma^2 * s, 4/sigma^2) and a seed reproduces its frames."""
+    import torch
+    from antpolarcodes_amd._native import Encoder, Plan, bpsk_awgn_device, random_info_device
+    N, K, F = 1024, 512, 4096
+    fr = oracle.frozen_bits_bb(N, K, 0.0)
+    tail = torch.empty((F, 65), dtype=torch.uint8, device="cuda:0")
+    random_info_device(tail, 516, seed=5)
+    t = tail.cpu().numpy()
+    assert (t[:, -1] & 0x0F).max() == 0 and t[:, -1].max() > 0 and t[:, :-1].std() > 60  # bits past K cleared
+    info = torch.empty((F, 64), dtype=torch.uint8, device="cuda:0")
+    random_info_device(info, K, seed=123)
+    code = torch.empty((F, N // 8), dtype=torch.uint8, device="cuda:0")
+    Encoder(N, fr, crc=8, device=0).encode_device(info, code)
+    llr = torch.empty((F, N), device="cuda:0")
+    bpsk_awgn_device(code, N, 0.0, 1, llr)
+    plan = Plan(N, 8, fr, crc=8, device=0)
+    out = torch.empty_like(info)
+    ok = torch.empty(F, dtype=torch.uint8, device="cuda:0")
+    plan.decode_device(llr, out, ok)
+    torch.cuda.synchronize()
+    assert torch.equal(out, info) and bool(ok.all())
+    sigma = 0.8
+    bpsk_awgn_device(code, N, sigma, 99, llr)
+    a = llr.cpu().numpy()
+    bpsk_awgn_device(code, N, sigma, 99, llr)
+    assert np.array_equal(a, llr.cpu().numpy())
+    s = 1.0 - 2.0 * np.unpackbits(code.cpu().numpy(), axis=1).astype(np.float32)
+    z = (a * sigma * sigma / 2.0 - s) / sigma
+    assert abs(z.mean()) < 5e-3 and abs(z.std() - 1.0) < 5e-3
+    assert abs((z ** 4).mean() - 3.0) < 0.05  # Gaussian kurtosis
