@@ -87,8 +87,8 @@ def test_decode_punctured_matches_oracle(oracle, L):
     bad = np.nonzero(~(gi == oi).all(axis=1))[0]
     assert bad.size == 0, f"frames {bad[:8]} differ"
     assert np.array_equal(d_ok.cpu().numpy(), ook)
-    # the channel was good enough that most frames decode (sanity, not parity)
-    assert (gi == info_tx).all(axis=1).mean() > 0.5
+    # sanity, not parity: SCL-8 decodes most frames at this SNR, SC some
+    assert (gi == info_tx).all(axis=1).mean() > (0.5 if L > 1 else 0.02)
 
 
 def test_nr_fixture_core_on_gpu():
