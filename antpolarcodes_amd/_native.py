@@ -71,6 +71,7 @@ def lib():
         L = C.CDLL(LIB_PATH)
         P = C.c_void_p
         L.pcg_plan_create.argtypes = [C.POINTER(P), C.c_uint32, C.c_uint32, P, C.c_uint32, C.c_int, C.c_int, C.c_int]
+        L.pcg_plan_create_adaptive.argtypes = L.pcg_plan_create.argtypes
         L.pcg_decode_f32.argtypes = [P, P, C.c_uint64, P, P, P, P]
         L.pcg_decode_f32_host.argtypes = [P, P, C.c_uint64, P, P, P]
         L.pcg_plan_describe.argtypes = [P, C.POINTER(PlanDesc)]
@@ -126,11 +127,14 @@ def _frozen_array(frozen):
 class Plan:
     """Owns one pcg_plan (decoder tree + device schedule for one device)."""
 
-    def __init__(self, N, L, frozen, systematic=True, crc=8, device=0):
+    def __init__(self, N, L, frozen, systematic=True, crc=8, device=0, adaptive=False):
+        """adaptive=True: Fast-SSC first, SCL-L for the frames whose check fails
+        (AdaptiveFloat, pcg_plan_create_adaptive)."""
         fr = np.ascontiguousarray(np.asarray(list(frozen), dtype=np.uint32))
         h = C.c_void_p()
-        _check(lib().pcg_plan_create(C.byref(h), int(N), int(L), fr.ctypes.data if fr.size else None,
-                                     int(fr.size), int(bool(systematic)), int(crc), int(device)))
+        create = lib().pcg_plan_create_adaptive if adaptive else lib().pcg_plan_create
+        _check(create(C.byref(h), int(N), int(L), fr.ctypes.data if fr.size else None,
+                      int(fr.size), int(bool(systematic)), int(crc), int(device)))
         self._h = h
         self.N, self.L, self.K = int(N), int(L), int(N) - int(fr.size)
         self.kb = (self.K + 7) // 8

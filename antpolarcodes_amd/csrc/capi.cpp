@@ -33,6 +33,12 @@ struct pcg_plan {
     // pcg_decode_punctured_f32: depunctured LLRs (F x N), reused across calls
     float* d_dep = nullptr;
     uint64_t dep_frames = 0;
+    // adaptive plans (pcg_plan_create_adaptive): the Fast-SSC first stage and the
+    // failed-frame list of the SCL second stage ([0] = count, then indices)
+    pcg_plan* fast = nullptr;
+    uint32_t* d_fmap = nullptr;
+    uint8_t* d_okbuf = nullptr;
+    uint64_t fmap_frames = 0;
 };
 
 namespace {
@@ -77,6 +83,8 @@ void free_plan_device(pcg_plan* p)
     (void)hipFree(p->d_ok);
     (void)hipFree(p->d_met);
     (void)hipFree(p->d_dep);
+    (void)hipFree(p->d_fmap);
+    (void)hipFree(p->d_okbuf);
 }
 
 } // namespace
@@ -189,6 +197,38 @@ int pcg_plan_create(pcg_plan** out,
     return PCG_OK;
 }
 
+int pcg_plan_create_adaptive(pcg_plan** out,
+                             uint32_t N,
+                             uint32_t L,
+                             const uint32_t* frozen,
+                             uint32_t n_frozen,
+                             int systematic,
+                             int crc_kind,
+                             int device)
+{
+    if (L < 2) // makeDecoder with listSize 1 builds the plain Fast-SSC decoder (decoder.cpp:60-68)
+        return pcg_plan_create(out, N, L, frozen, n_frozen, systematic, crc_kind, device);
+    int rc = pcg_plan_create(out, N, L, frozen, n_frozen, systematic, crc_kind, device);
+    if (rc != 0)
+        return rc;
+    if ((*out)->host.scl_kind != 0) {
+        pcg_plan_destroy(*out);
+        *out = nullptr;
+        return fail(PCG_E_UNSUPPORTED, "adaptive decoding needs the lane-serial SCL kernel");
+    }
+    pcg_plan* fast = nullptr;
+    // the Fast-SSC stage rejects what FastSscAvxFloat's constructor rejects (invalid_argument)
+    rc = pcg_plan_create(&fast, N, 1, frozen, n_frozen, systematic, crc_kind, device);
+    if (rc != 0) {
+        std::string msg = g_last_error;
+        pcg_plan_destroy(*out);
+        *out = nullptr;
+        return fail(rc, msg);
+    }
+    (*out)->fast = fast;
+    return PCG_OK;
+}
+
 int pcg_plan_describe(const pcg_plan* p, pcg_plan_desc* d)
 {
     if (!p || !d)
@@ -203,6 +243,44 @@ int pcg_plan_describe(const pcg_plan* p, pcg_plan_desc* d)
     d->crc_kind = p->host.crc_kind;
     d->systematic = p->host.systematic;
     return PCG_OK;
+}
+
+static int decode_impl(pcg_plan* p,
+                       const float* llr,
+                       uint64_t F,
+                       uint8_t* info,
+                       uint8_t* ok,
+                       float* metrics,
+                       void* stream,
+                       const uint32_t* fmap,
+                       const uint32_t* fcount);
+
+static int decode_adaptive(pcg_plan* p, const float* llr, uint64_t F, uint8_t* info, uint8_t* ok, float* metrics,
+                           void* stream)
+{
+    // AdaptiveFloat::decode (adaptive_float.cpp:33-45): Fast-SSC for every frame, then SCL
+    // for the frames whose check failed, whose SCL output (and ok) replaces the SC one.
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    hipError_t e;
+    if (p->fmap_frames < F) {
+        (void)hipFree(p->d_fmap);
+        (void)hipFree(p->d_okbuf);
+        p->d_fmap = nullptr;
+        p->d_okbuf = nullptr;
+        p->fmap_frames = 0;
+        if ((e = hipMalloc(&p->d_fmap, 4 * (F + 1))) != hipSuccess || (e = hipMalloc(&p->d_okbuf, F)) != hipSuccess)
+            return hip_fail(e, "hipMalloc(adaptive)");
+        p->fmap_frames = F;
+    }
+    uint8_t* okb = ok ? ok : p->d_okbuf;
+    int rc = decode_impl(p->fast, llr, F, info, okb, nullptr, stream, nullptr, nullptr);
+    if (rc != 0)
+        return rc;
+    if (metrics && (e = hipMemsetAsync(metrics, 0, F * p->host.L * sizeof(float), s)) != hipSuccess)
+        return hip_fail(e, "hipMemsetAsync(metrics)");
+    if (pcg::launch_compact_failed(okb, F, p->d_fmap + 1, p->d_fmap, s) != 0)
+        return fail(PCG_E_HIP, std::string("compaction launch failed: ") + hipGetErrorString(hipGetLastError()));
+    return decode_impl(p, llr, F, info, okb, metrics, stream, p->d_fmap + 1, p->d_fmap);
 }
 
 int pcg_decode_f32(pcg_plan* p,
@@ -221,7 +299,24 @@ int pcg_decode_f32(pcg_plan* p,
         return fail(PCG_E_ARG, "null llr/info buffer");
     if (p->device < 0)
         return fail(PCG_E_NODEVICE, "host-only plan (created with device < 0)");
+    if (F > 0xFFFFFFFFull)
+        return fail(PCG_E_ARG, "at most 2^32 - 1 frames per call");
     DeviceGuard g(p->device);
+    if (p->fast)
+        return decode_adaptive(p, llr, F, info, ok, metrics, stream);
+    return decode_impl(p, llr, F, info, ok, metrics, stream, nullptr, nullptr);
+}
+
+static int decode_impl(pcg_plan* p,
+                       const float* llr,
+                       uint64_t F,
+                       uint8_t* info,
+                       uint8_t* ok,
+                       float* metrics,
+                       void* stream,
+                       const uint32_t* fmap,
+                       const uint32_t* fcount)
+{
     const auto& h = p->host;
     pcg::KernelArgs a{};
     a.llr = llr;
@@ -246,6 +341,8 @@ int pcg_decode_f32(pcg_plan* p,
     a.lds_stage_limit = p->lds_stage_limit;
     a.scl_virt = p->scl_virt;
     a.scratch_floats = p->scratch_floats;
+    a.fmap = fmap;
+    a.fcount = fcount;
     if (getenv("PCG_OPPROF")) {
         if (!g_prof && hipMalloc(&g_prof, 128 * sizeof(unsigned long long)) == hipSuccess)
             (void)hipMemset(g_prof, 0, 128 * sizeof(unsigned long long));
@@ -383,6 +480,7 @@ void pcg_plan_destroy(pcg_plan* p)
 {
     if (!p)
         return;
+    pcg_plan_destroy(p->fast);
     if (p->device >= 0) {
         DeviceGuard g(p->device);
         free_plan_device(p);

@@ -30,6 +30,8 @@ int launch_puncture(const float* in, uint64_t F, uint32_t N, uint32_t E, const u
 int launch_puncture_packed(const uint8_t* in, uint64_t F, uint32_t N, uint32_t E, const uint32_t* pos, uint8_t* out,
                            hipStream_t s);
 int launch_encode(const EncodeArgs& a, hipStream_t s);
+// adaptive decoding: indices of frames with ok == 0 into fmap, their number into *count
+int launch_compact_failed(const uint8_t* ok, uint64_t F, uint32_t* fmap, uint32_t* count, hipStream_t s);
 int launch_random_info(uint8_t* info, uint64_t F, uint32_t K, uint64_t seed, hipStream_t s);
 int launch_bpsk_awgn(const uint8_t* code, uint64_t F, uint32_t n, float sigma, uint64_t seed, float* llr,
                      hipStream_t s);

@@ -308,7 +308,42 @@ __global__ void __launch_bounds__(kBlock) bpsk_awgn_kernel(const uint8_t* __rest
     }
 }
 
+// ---- adaptive decoding: the frames whose first-stage check failed ---------------------------
+// fmap[0 .. *count) = { f : ok[f] == 0 } (any order; *count zeroed by the caller).  One atomic
+// per wave: ballot, popcount, lane-prefix.
+__global__ void __launch_bounds__(kBlock) compact_failed_kernel(const uint8_t* __restrict__ ok,
+                                                               uint64_t F,
+                                                               uint32_t* __restrict__ fmap,
+                                                               uint32_t* __restrict__ count)
+{
+    const uint32_t lane = lane_id();
+    for (uint64_t base = ((uint64_t)blockIdx.x * kBlock + (threadIdx.x & ~63u)); base < F;
+         base += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t f = base + lane;
+        const bool fail = f < F && ok[f] == 0;
+        const uint64_t m = ballot(fail);
+        if (m == 0)
+            continue;
+        uint32_t off = 0;
+        if (lane == 0)
+            off = atomicAdd(count, (uint32_t)__builtin_popcountll(m));
+        off = __shfl(off, 0, 64);
+        if (fail)
+            fmap[off + (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull))] = (uint32_t)f;
+    }
+}
+
 } // namespace
+
+int launch_compact_failed(const uint8_t* ok, uint64_t F, uint32_t* fmap, uint32_t* count, hipStream_t s)
+{
+    if (hipMemsetAsync(count, 0, sizeof(uint32_t), s) != hipSuccess)
+        return -3;
+    if (F == 0)
+        return 0;
+    hipLaunchKernelGGL(compact_failed_kernel, dim3(grid_for(F, kBlock)), dim3(kBlock), 0, s, ok, F, fmap, count);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
 
 int launch_depuncture(const float* in, uint64_t F, uint32_t E, uint32_t N, const int32_t* src, float* out,
                       hipStream_t s)

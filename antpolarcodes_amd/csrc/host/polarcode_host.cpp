@@ -391,11 +391,18 @@ void GpuDecoder::initialize(size_t blockLength, const std::vector<unsigned>& fro
     releasePlan();
     // validate (and classify) now so invalid codes fail at construction like the reference
     pcg_plan* probe = nullptr;
-    const int rc = pcg_plan_create(&probe, (uint32_t)blockLength, (uint32_t)mListSize, mFrozenBits.data(),
-                                   (uint32_t)mFrozenBits.size(), 1, 0, -1);
+    int rc = pcg_plan_create(&probe, (uint32_t)blockLength, (uint32_t)mListSize, mFrozenBits.data(),
+                             (uint32_t)mFrozenBits.size(), 1, 0, -1);
     if (rc != 0)
         throw_pcg(rc);
     pcg_plan_destroy(probe);
+    if (mAdaptive) { // AdaptiveFloat also constructs a FastSscAvxFloat (adaptive_float.cpp:23)
+        rc = pcg_plan_create(&probe, (uint32_t)blockLength, 1, mFrozenBits.data(), (uint32_t)mFrozenBits.size(), 1,
+                             0, -1);
+        if (rc != 0)
+            throw_pcg(rc);
+        pcg_plan_destroy(probe);
+    }
 }
 
 void GpuDecoder::setSystematic(bool sys) { mSystematic = sys; }
@@ -413,8 +420,9 @@ void GpuDecoder::ensurePlan()
     if (mPlan && kind == mPlanKind && mSystematic == mPlanSys)
         return;
     releasePlan();
-    const int rc = pcg_plan_create(&mPlan, (uint32_t)mBlockLength, (uint32_t)mListSize, mFrozenBits.data(),
-                                   (uint32_t)mFrozenBits.size(), mSystematic ? 1 : 0, kind, mDevice);
+    auto create = mAdaptive ? pcg_plan_create_adaptive : pcg_plan_create;
+    const int rc = create(&mPlan, (uint32_t)mBlockLength, (uint32_t)mListSize, mFrozenBits.data(),
+                          (uint32_t)mFrozenBits.size(), mSystematic ? 1 : 0, kind, mDevice);
     if (rc != 0) {
         mPlan = nullptr;
         throw_pcg(rc);
@@ -458,11 +466,24 @@ void GpuDecoder::decodeBatchDevice(const float* llr, size_t F, uint8_t* info, ui
         throw_pcg(rc);
 }
 
-Decoder* makeDecoder(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits, int)
+GpuAdaptiveFloat::GpuAdaptiveFloat(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,
+                                   int device)
+    : GpuDecoder(blockLength, listSize, {}, device)
+{
+    mAdaptive = true;
+    initialize(blockLength, frozenBits); // validate both stages now (GpuDecoder's ran before mAdaptive)
+}
+
+Decoder* makeDecoder(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits, int impl)
 {
     Decoder* dec;
+    if (impl != 1 && impl != 2)
+        throw std::logic_error("decoder implementation " + std::to_string(impl) +
+                               " (char / SCAN) is not part of this build (use \"gpu\")");
     if (listSize <= 1)
         dec = new GpuFastSscFloat(blockLength, frozenBits);
+    else if (impl == 2)
+        dec = new GpuAdaptiveFloat(blockLength, listSize, frozenBits);
     else
         dec = new GpuSclFloat(blockLength, listSize, frozenBits);
     dec->setErrorDetection(new ErrorDetection::CRC8()); // decoder.cpp:85 (never freed there either)
@@ -472,11 +493,13 @@ Decoder* makeDecoder(size_t blockLength, size_t listSize, const std::vector<unsi
 Decoder* create(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits, std::string type)
 {
     std::transform(type.begin(), type.end(), type.begin(), [](unsigned char c) { return std::tolower(c); });
+    // decoder.cpp:35-51: "char" is tested first, then "float", "mixed", "scan"
+    if (type.find("char") != std::string::npos || type.find("scan") != std::string::npos)
+        throw std::logic_error("PolarDecoder type '" + type + "' is not part of this build (use \"gpu\")");
     if (type.find("gpu") != std::string::npos || type.find("float") != std::string::npos)
         return makeDecoder(blockLength, listSize, frozenBits, 1);
-    if (type.find("char") != std::string::npos || type.find("mixed") != std::string::npos ||
-        type.find("scan") != std::string::npos)
-        throw std::logic_error("PolarDecoder type '" + type + "' is not part of this build (use \"gpu\")");
+    if (type.find("mixed") != std::string::npos)
+        return makeDecoder(blockLength, listSize, frozenBits, 2);
     throw std::logic_error("Unknown PolarDecoder type!");
 }
 

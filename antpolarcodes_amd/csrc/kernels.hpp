@@ -27,6 +27,10 @@ struct KernelArgs {
     unsigned long long* prof; // dev-only: per-op-code [cycles, count] (null = off)
     uint32_t flags;           // dev-only experiment switches (PCG_FLAGS), 0 in production
     uint32_t scl_virt;        // lane-serial SCL: top stages recomputed instead of stored (0..2)
+    // lane-serial SCL only: decode frames fmap[0 .. *fcount) (device) instead of 0 .. F-1
+    // (the adaptive decoder's second stage; F bounds *fcount and sizes the grid)
+    const uint32_t* fmap;
+    const uint32_t* fcount;
 };
 
 // LDS floats one SC codeword needs: alpha (N floats, index 0 unused) + packed bits.

@@ -1163,10 +1163,13 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
     c.gs = a.scratch + (uint64_t)blockIdx.x * a.scratch_floats;
     const uint32_t W = a.N >= 32 ? a.N / 32 : 1u;
 
-    for (uint64_t fb = (uint64_t)blockIdx.x * G; fb < a.F; fb += (uint64_t)gridDim.x * G) {
-        const uint64_t frame = fb + c.lane / LP;
-        const bool fvalid = frame < a.F;
-        c.y = a.llr + (fvalid ? frame : a.F - 1) * a.N;
+    const uint64_t Fn = a.fcount ? (uint64_t)*a.fcount : a.F;
+    for (uint64_t fb = (uint64_t)blockIdx.x * G; fb < Fn; fb += (uint64_t)gridDim.x * G) {
+        const uint64_t slot = fb + c.lane / LP;
+        const bool fvalid = slot < Fn;
+        const uint64_t fs = fvalid ? slot : Fn - 1;
+        const uint64_t frame = a.fmap ? (uint64_t)a.fmap[fs] : fs;
+        c.y = a.llr + frame * a.N;
         c.m = 0.0f; // a freshly constructed decoder
         c.ptr = 0;
         uint32_t P = 1;

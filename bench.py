@@ -8,7 +8,7 @@ and checked by the decoder) through the C ABI (pcg_decode_f32) on the GPU.  Ever
 rank decodes its own batch (independent frames shard with no collective:
 weak scaling); the barrier/max-reduction uses gloo on the host.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--mode scl8|sc|scl32]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--mode scl8|sc|scl32|nr5g|adaptive8]
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -27,6 +27,8 @@ MODES = {
     "scl32": (4096, 2048, 32, 1 << 14, "config 5 shard shape: SCL L=32, N=4096 K=2048, 2^14 frames/GPU"),
     "nr5g": (1024, 512, 8, 1 << 16, "config 4: 5G NR uplink, FiveGList N=1024 K=512 (501 + CRC-11), "
                                      "punctured to E=896, device depuncture + SCL L=8, 2^16 frames"),
+    "adaptive8": (1024, 512, 8, 1 << 16, "config 3 with the adaptive decoder (AdaptiveFloat): Fast-SSC, "
+                                         "then SCL L=8 for CRC-8 failures, N=1024 K=512, 2^16 frames"),
 }
 NR_E = 896
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured float4 copy)
@@ -101,7 +103,7 @@ def main():
     else:
         frozen = frozen_bits(N, K, 0.0, "BB")
         llr, info, _ = frames.awgn_frames(N, frozen, F, args.ebn0, seed=1000 + rank, crc=crc)
-    plan = Plan(N, L, frozen, systematic=True, crc=crc, device=local)
+    plan = Plan(N, L, frozen, systematic=True, crc=crc, device=local, adaptive=args.mode == "adaptive8")
     kb = plan.kb
     d_llr = torch.from_numpy(llr).to(f"cuda:{local}")
     d_info = torch.empty((F, kb), dtype=torch.uint8, device=f"cuda:{local}")

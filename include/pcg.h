@@ -18,6 +18,8 @@
  *   pcg_decode_f32    <- Decoder::decode_vector(const float*, void*) decoder.cpp:154-167,
  *                        batched: F frames per call, device-resident buffers
  *   pcg_decode_f32_host <- the same with host buffers (H2D + decode + D2H)
+ *   pcg_plan_create_adaptive <- makeDecoder(..., 2) = AdaptiveFloat, decoder.cpp:75,
+ *                        adaptive_float.cpp:14-45 (SC first, SCL for the failures)
  *   pcg_plan_destroy  <- Decoder::~Decoder decoder.cpp:104-114
  *   pcg_last_error    <- the std::exception text the reference throws
  *   pcg_puncturer_*   <- PolarCode::Puncturer (include/polarcode/puncturer.h:33-99,
@@ -89,6 +91,22 @@ int pcg_plan_create(pcg_plan** plan,
                     int systematic,
                     int crc_kind,
                     int device);
+
+/* An adaptive plan (makeDecoder's "mixed" = AdaptiveFloat, decoder.cpp:40-41, 75;
+ * adaptive_float.cpp:33-45): pcg_decode_f32 first decodes every frame with Fast-SSC, then
+ * re-decodes the frames whose detector check failed with CRC-aided SCL (list size L); a
+ * re-decoded frame reports the SCL output and ok flag.  metrics: the SCL path metrics of
+ * re-decoded frames, 0 for frames Fast-SSC settled.  Asynchronous (the failed-frame list
+ * stays on the device).  L < 2 creates a plain Fast-SSC plan.  Fails like both decoders'
+ * constructors (PCG_E_FROZEN for frozen patterns Fast-SSC rejects). */
+int pcg_plan_create_adaptive(pcg_plan** plan,
+                             uint32_t N,
+                             uint32_t L,
+                             const uint32_t* frozen,
+                             uint32_t n_frozen,
+                             int systematic,
+                             int crc_kind,
+                             int device);
 
 /* Decode F frames.  llr: device pointer, F x N float32 (natural order, LLR > 0
  * <=> bit 0).  info: device pointer, F x ceil(K/8) bytes (MSB-first info bits,

@@ -81,6 +81,7 @@ protected:
     pcg_plan* mPlan = nullptr;
     int mPlanKind = -2;
     bool mPlanSys = true;
+    bool mAdaptive = false; ///< pcg_plan_create_adaptive (Fast-SSC first, SCL for failures)
     void ensurePlan();
     void releasePlan();
 
@@ -122,6 +123,17 @@ public:
 
 /// makeDecoder (decoder.cpp:54-87): L == 1 -> Fast-SSC, else SCL; always installs
 /// a CRC-8 detector (the reference's Q5 behaviour).
+/// AdaptiveFloat (adaptive_float.cpp:14-45): Fast-SSC, then CRC-aided SCL for the frames
+/// whose check fails -- per frame, on the GPU, in one batched call.
+class GpuAdaptiveFloat : public GpuDecoder
+{
+public:
+    GpuAdaptiveFloat(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,
+                     int device = 0);
+};
+
+/// decoder_impl as in decoder.cpp:54-87: 1 = float (Fast-SSC / SCL), 2 = AdaptiveFloat
+/// (list size >= 2); the "char" (0) and SCAN (3) implementations are not part of this build.
 Decoder* makeDecoder(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,
                      int decoder_impl = 1);
 

@@ -71,3 +71,28 @@ def test_decoder_construction_and_errors(pp):
     # Fast-SSC rejects the frozen patterns the reference rejects (std::invalid_argument)
     with pytest.raises(ValueError):
         pp.PolarDecoder(8, 1, [1, 2, 4], "gpu")
+
+
+def test_mixed_is_adaptive_float():
+    """create(..., "mixed") -> AdaptiveFloat (decoder.cpp:40-41, 75): constructs both stages,
+    so frozen patterns Fast-SSC rejects fail for it too, while "float" SCL accepts them."""
+    from antpolarcodes_amd import pypolar as pp
+    fr = pp.frozen_bits(1024, 512, 0.0)
+    dec = pp.PolarDecoder(1024, 8, fr, "Mixed")
+    assert dec.listSize() == 8 and dec.getErrorDetectionMode() == "CRC-8"
+    assert pp.PolarDecoder(1024, 1, fr, "mixed").listSize() == 1
+    pp.PolarDecoder(8, 4, [1, 2, 4], "float")
+    with pytest.raises(ValueError):
+        pp.PolarDecoder(8, 4, [1, 2, 4], "mixed")
+    with pytest.raises(RuntimeError, match="not part of this build"):
+        pp.PolarDecoder(1024, 8, fr, "char")
+
+
+def test_adaptive_plan_host_only():
+    from antpolarcodes_amd import _native as nat
+    fr = list(range(32))
+    d = nat.Plan(64, 8, fr, adaptive=True, device=-1).describe()
+    assert d["list_size"] == 8
+    with pytest.raises(nat.PcgError) as e:
+        nat.Plan(8, 4, [1, 2, 4], adaptive=True, device=-1)
+    assert e.value.code == nat.PCG_E_FROZEN
