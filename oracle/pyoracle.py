@@ -53,6 +53,16 @@ class Oracle:
         lib.orc_depuncture.restype = None
         lib.orc_puncture_packed.argtypes = [_U32, _P, _P, _P]
         lib.orc_puncture_packed.restype = None
+        # int8 ("char") decoders, polar_oracle_char.c
+        lib.orc_f32_to_i8.argtypes = [_P, _U32, _U64, _P]
+        lib.orc_f32_to_i8.restype = None
+        lib.orc_scc_decode.argtypes = [_U32, _P, _U32, _I, _I, _P, _U64, _P, _P, _P]
+        lib.orc_sclc_decode.argtypes = [_U32, _U32, _P, _U32, _I, _I, _I, _P, _U64, _P, _P, _P, _P, _P]
+        lib.orc_scc_tree.argtypes = [_U32, _P, _U32, _P, _P, _I]
+        lib.orc_sclc_tree.argtypes = [_U32, _P, _U32, _P, _P, _I]
+        for fn, n in (("orc_fip_f", 3), ("orc_fip_g", 4), ("orc_fip_combine_short", 4)):
+            getattr(lib, fn).argtypes = [_P] * (n - 1) + [_U32]
+            getattr(lib, fn).restype = None
         self.lib = lib
 
     def f(self, left, right):
@@ -163,6 +173,84 @@ class Oracle:
         llr = np.ascontiguousarray(llr, dtype=np.float32).reshape(-1, N)
         return self.lib.orc_bench(N, L, _p(fr), len(fr), _p(llr), llr.shape[0], reps)
 
+    # ---- int8 ("char") decoders ------------------------------------------------------
+    def f32_to_i8(self, llr, N):
+        """CharContainer::insertLlr(const float*) for frames of N floats."""
+        x = np.ascontiguousarray(llr, np.float32).reshape(-1, N)
+        out = np.zeros(x.shape, np.int8)
+        self.lib.orc_f32_to_i8(_p(x), N, x.shape[0], _p(out))
+        return out
+
+    def _i8(self, llr, N):
+        llr = np.asarray(llr)
+        if llr.dtype != np.int8:
+            return self.f32_to_i8(llr, N)
+        return np.ascontiguousarray(llr).reshape(-1, N)
+
+    def scc_decode(self, N, frozen, llr, systematic=True, crc=-1, soft=False):
+        """FastSscFipChar; llr int8 (or float, quantised as insertLlr does)."""
+        fr = _frozen(frozen)
+        llr = self._i8(llr, N)
+        F = llr.shape[0]
+        kb = (N - len(fr) + 7) // 8
+        info = np.zeros((F, kb), np.uint8)
+        ok = np.zeros(F, np.uint8)
+        cw = np.zeros((F, N), np.int8) if soft else None
+        r = self.lib.orc_scc_decode(N, _p(fr), len(fr), int(systematic), crc, _p(llr), F,
+                                    _p(info), _p(ok), _p(cw))
+        if r != 0:
+            raise ValueError(f"orc_scc_decode failed ({r})")
+        return (info, ok, cw) if soft else (info, ok)
+
+    def sclc_decode(self, N, L, frozen, llr, systematic=True, crc=-1, carry=False, paths=False):
+        """SclFipChar; metrics are int64."""
+        fr = _frozen(frozen)
+        llr = self._i8(llr, N)
+        F = llr.shape[0]
+        kb = (N - len(fr) + 7) // 8
+        info = np.zeros((F, kb), np.uint8)
+        ok = np.zeros(F, np.uint8)
+        met = np.zeros((F, L), np.int64) if paths else None
+        pc = np.zeros(F, np.uint32) if paths else None
+        pb = np.zeros((F, L, N // 8), np.uint8) if paths else None
+        r = self.lib.orc_sclc_decode(N, L, _p(fr), len(fr), int(systematic), crc, int(carry),
+                                     _p(llr), F, _p(info), _p(ok), _p(met), _p(pc), _p(pb))
+        if r != 0:
+            raise ValueError(f"orc_sclc_decode failed ({r})")
+        return (info, ok, met, pc, pb) if paths else (info, ok)
+
+    def fip_f(self, left, right):
+        x = np.ascontiguousarray(np.concatenate([left, right]), np.int8)
+        h = len(left)
+        out = np.zeros(max(h, 32), np.int8)
+        self.lib.orc_fip_f(_p(x), _p(out), h)
+        return out[:h]
+
+    def fip_g(self, left, right, bits):
+        x = np.ascontiguousarray(np.concatenate([left, right]), np.int8)
+        b = np.ascontiguousarray(bits, np.int8)
+        h = len(left)
+        out = np.zeros(max(h, 32), np.int8)
+        self.lib.orc_fip_g(_p(x), _p(b), _p(out), h)
+        return out[:h]
+
+    def fip_combine_short(self, left, right, h):
+        l = np.array(left, np.int8)
+        r = np.array(right, np.int8)
+        out = np.zeros(32, np.int8)
+        self.lib.orc_fip_combine_short(_p(l), _p(r), _p(out), h)
+        return out
+
+    def char_tree(self, N, frozen, L=1):
+        fr = _frozen(frozen)
+        t = np.zeros(4 * N, np.int32)
+        s = np.zeros(4 * N, np.int32)
+        fn = self.lib.orc_scc_tree if L == 1 else self.lib.orc_sclc_tree
+        k = fn(N, _p(fr), len(fr), _p(t), _p(s), 4 * N)
+        if k < 0:
+            raise ValueError(f"invalid frozen set ({k})")
+        return t[:k], s[:k]
+
 
 class Reference:
     """The reference library itself (only where oracle/_ref was built)."""
@@ -181,6 +269,11 @@ class Reference:
         lib.ref_last_error.restype = C.c_char_p
         lib.ref_puncturer.argtypes = [_U32, _P, _U32, _P, _P]
         lib.ref_punc_apply.argtypes = [_U32, _P, _U32, _I, _P, _P]
+        lib.ref_f32_to_i8.argtypes = [_U32, _P, _U64, _P]
+        lib.ref_decode_char.argtypes = [_U32, _U32, _P, _U32, _I, _I, _I, _P, _U64, _P, _P, _P]
+        lib.ref_sclc_paths.argtypes = [_U32, _U32, _P, _U32, _P, _U64, _P, _P, _P]
+        lib.ref_bench_char.argtypes = [_U32, _U32, _P, _U32, _I, _I, _P, _U64, _I, _I]
+        lib.ref_bench_char.restype = C.c_double
         self.lib = lib
 
     @staticmethod
@@ -277,3 +370,51 @@ class Reference:
         llr = np.ascontiguousarray(llr, dtype=np.float32).reshape(-1, N)
         return self.lib.ref_bench(N, L, _p(fr), len(fr), int(systematic), crc, _p(llr), llr.shape[0],
                                   threads, reps)
+
+    # ---- int8 ("char") decoders ------------------------------------------------------
+    def f32_to_i8(self, llr, N):
+        x = np.ascontiguousarray(llr, np.float32).reshape(-1, N)
+        out = np.zeros(x.shape, np.int8)
+        if self.lib.ref_f32_to_i8(N, _p(x), x.shape[0], _p(out)) != 0:
+            raise ValueError(self.lib.ref_last_error().decode())
+        return out
+
+    def decode_char(self, N, L, frozen, llr, systematic=True, crc=-1, soft=False, fresh=False):
+        """create(N, L, frozen, "char"): int8 llr -> decode_vector(const char*), float llr ->
+        decode_vector(const float*).  fresh=True: one decoder per frame."""
+        fr = _frozen(frozen)
+        llr = np.asarray(llr)
+        is_i8 = llr.dtype == np.int8
+        llr = np.ascontiguousarray(llr, dtype=np.int8 if is_i8 else np.float32).reshape(-1, N)
+        F = llr.shape[0]
+        kb = (N - len(fr) + 7) // 8
+        info = np.zeros((F, kb), np.uint8)
+        ok = np.zeros(F, np.uint8)
+        cw = np.zeros((F, N), np.int8) if soft else None
+        rng = [(f, f + 1) for f in range(F)] if fresh else [(0, F)]
+        for a, b in rng:
+            r = self.lib.ref_decode_char(N, L, _p(fr), len(fr), int(systematic), crc, int(is_i8),
+                                         _p(llr[a:b]), b - a, _p(info[a:b]), _p(ok[a:b]),
+                                         None if cw is None else _p(cw[a:b]))
+            if r != 0:
+                raise ValueError(self.lib.ref_last_error().decode())
+        return (info, ok, cw) if soft else (info, ok)
+
+    def sclc_paths(self, N, L, frozen, llr):
+        """SclFip internals, fresh path list per frame: int64 metrics, counts, path bits."""
+        fr = _frozen(frozen)
+        llr = np.ascontiguousarray(llr, dtype=np.int8).reshape(-1, N)
+        F = llr.shape[0]
+        met = np.zeros((F, L), np.int64)
+        pc = np.zeros(F, np.uint32)
+        pb = np.zeros((F, L, N // 8), np.uint8)
+        r = self.lib.ref_sclc_paths(N, L, _p(fr), len(fr), _p(llr), F, _p(met), _p(pc), _p(pb))
+        if r != 0:
+            raise ValueError(self.lib.ref_last_error().decode())
+        return met, pc, pb
+
+    def bench_char(self, N, L, frozen, llr, threads=1, reps=1, systematic=True, crc=-1):
+        fr = _frozen(frozen)
+        llr = np.ascontiguousarray(llr, dtype=np.int8).reshape(-1, N)
+        return self.lib.ref_bench_char(N, L, _p(fr), len(fr), int(systematic), crc, _p(llr),
+                                       llr.shape[0], threads, reps)
