@@ -72,6 +72,9 @@ def lib():
         P = C.c_void_p
         L.pcg_plan_create.argtypes = [C.POINTER(P), C.c_uint32, C.c_uint32, P, C.c_uint32, C.c_int, C.c_int, C.c_int]
         L.pcg_plan_create_adaptive.argtypes = L.pcg_plan_create.argtypes
+        L.pcg_plan_create_char.argtypes = L.pcg_plan_create.argtypes
+        L.pcg_decode_i8.argtypes = [P, P, C.c_uint64, P, P, P, P]
+        L.pcg_decode_i8_host.argtypes = [P, P, C.c_uint64, P, P, P]
         L.pcg_decode_f32.argtypes = [P, P, C.c_uint64, P, P, P, P]
         L.pcg_decode_f32_host.argtypes = [P, P, C.c_uint64, P, P, P]
         L.pcg_plan_describe.argtypes = [P, C.POINTER(PlanDesc)]
@@ -127,18 +130,23 @@ def _frozen_array(frozen):
 class Plan:
     """Owns one pcg_plan (decoder tree + device schedule for one device)."""
 
-    def __init__(self, N, L, frozen, systematic=True, crc=8, device=0, adaptive=False):
+    def __init__(self, N, L, frozen, systematic=True, crc=8, device=0, adaptive=False, fixed=False):
         """adaptive=True: Fast-SSC first, SCL-L for the frames whose check fails
-        (AdaptiveFloat, pcg_plan_create_adaptive)."""
+        (AdaptiveFloat, pcg_plan_create_adaptive).  fixed=True: the reference's 8-bit
+        decoders FastSscFipChar / SclFipChar (pcg_plan_create_char)."""
         fr = np.ascontiguousarray(np.asarray(list(frozen), dtype=np.uint32))
         h = C.c_void_p()
-        create = lib().pcg_plan_create_adaptive if adaptive else lib().pcg_plan_create
+        if adaptive and fixed:
+            raise ValueError("the adaptive decoder is float only (AdaptiveFloat)")
+        create = (lib().pcg_plan_create_adaptive if adaptive else
+                  lib().pcg_plan_create_char if fixed else lib().pcg_plan_create)
         _check(create(C.byref(h), int(N), int(L), fr.ctypes.data if fr.size else None,
                       int(fr.size), int(bool(systematic)), int(crc), int(device)))
         self._h = h
         self.N, self.L, self.K = int(N), int(L), int(N) - int(fr.size)
         self.kb = (self.K + 7) // 8
         self.device = device
+        self.fixed = bool(fixed)
 
     def describe(self):
         d = PlanDesc()
@@ -155,6 +163,23 @@ class Plan:
                                          None if ok is None else ok.ctypes.data,
                                          None if met is None else met.ctypes.data))
         return info, ok, met
+
+    def decode_host_i8(self, llr, want_ok=True, want_metrics=False):
+        """int8 frames (8-bit plans): pcg_decode_i8_host."""
+        llr = np.ascontiguousarray(llr, dtype=np.int8).reshape(-1, self.N)
+        F = llr.shape[0]
+        info = np.zeros((F, self.kb), np.uint8)
+        ok = np.zeros(F, np.uint8) if want_ok else None
+        met = np.zeros((F, self.L), np.float32) if want_metrics else None
+        _check(lib().pcg_decode_i8_host(self._h, llr.ctypes.data, F, info.ctypes.data,
+                                        None if ok is None else ok.ctypes.data,
+                                        None if met is None else met.ctypes.data))
+        return info, ok, met
+
+    def decode_device_i8(self, llr, info, ok=None, metrics=None, stream=None):
+        """int8 device frames (torch.int8 tensors or raw pointers): pcg_decode_i8."""
+        _check(lib().pcg_decode_i8(self._h, _ptr(llr), llr.shape[0], _ptr(info), _ptr(ok), _ptr(metrics),
+                                   _stream(stream, llr)))
 
     def decode_device(self, llr, info, ok=None, metrics=None, stream=None):
         """Device-resident decode; arguments are torch CUDA tensors (or raw ints)."""

@@ -121,26 +121,37 @@ int pcg_device_count(void)
     return n;
 }
 
-int pcg_plan_create(pcg_plan** out,
-                    uint32_t N,
-                    uint32_t L,
-                    const uint32_t* frozen,
-                    uint32_t n_frozen,
-                    int systematic,
-                    int crc_kind,
-                    int device)
+static int plan_create_impl(pcg_plan** out,
+                            uint32_t N,
+                            uint32_t L,
+                            const uint32_t* frozen,
+                            uint32_t n_frozen,
+                            int systematic,
+                            int crc_kind,
+                            int device,
+                            int fixed)
 {
     if (!out)
         return fail(PCG_E_ARG, "plan output pointer is null");
     *out = nullptr;
     auto* p = new pcg_plan();
     std::string err;
-    int rc = pcg::build_plan(p->host, N, L, frozen, n_frozen, systematic, crc_kind, &err);
+    int rc = pcg::build_plan(p->host, N, L, frozen, n_frozen, systematic, crc_kind, &err, fixed);
     if (rc != 0) {
         delete p;
         return fail(rc, err);
     }
-    if (L == 1) {
+    if (fixed && L == 1) {
+        p->wave_lds_floats = pcg::sc_wave_lds_floats(N);
+    } else if (fixed) {
+        uint64_t sd = 0;
+        rc = pcg::sclc_layout(N, L, &p->wave_lds_floats, &p->lds_stage_limit, &sd);
+        if (rc != 0) {
+            delete p;
+            return fail(rc, "8-bit list decoding layout unsupported for this N/L");
+        }
+        p->scratch_floats = sd;
+    } else if (L == 1) {
         p->wave_lds_floats = pcg::sc_wave_lds_floats(N);
     } else {
         rc = p->host.scl_kind == 0
@@ -195,6 +206,30 @@ int pcg_plan_create(pcg_plan** out,
     }
     *out = p;
     return PCG_OK;
+}
+
+int pcg_plan_create(pcg_plan** out,
+                    uint32_t N,
+                    uint32_t L,
+                    const uint32_t* frozen,
+                    uint32_t n_frozen,
+                    int systematic,
+                    int crc_kind,
+                    int device)
+{
+    return plan_create_impl(out, N, L, frozen, n_frozen, systematic, crc_kind, device, 0);
+}
+
+int pcg_plan_create_char(pcg_plan** out,
+                         uint32_t N,
+                         uint32_t L,
+                         const uint32_t* frozen,
+                         uint32_t n_frozen,
+                         int systematic,
+                         int crc_kind,
+                         int device)
+{
+    return plan_create_impl(out, N, L, frozen, n_frozen, systematic, crc_kind, device, 1);
 }
 
 int pcg_plan_create_adaptive(pcg_plan** out,
@@ -253,7 +288,8 @@ static int decode_impl(pcg_plan* p,
                        float* metrics,
                        void* stream,
                        const uint32_t* fmap,
-                       const uint32_t* fcount);
+                       const uint32_t* fcount,
+                       const int8_t* llr8 = nullptr);
 
 static int decode_adaptive(pcg_plan* p, const float* llr, uint64_t F, uint8_t* info, uint8_t* ok, float* metrics,
                            void* stream)
@@ -315,7 +351,8 @@ static int decode_impl(pcg_plan* p,
                        float* metrics,
                        void* stream,
                        const uint32_t* fmap,
-                       const uint32_t* fcount)
+                       const uint32_t* fcount,
+                       const int8_t* llr8)
 {
     const auto& h = p->host;
     pcg::KernelArgs a{};
@@ -343,6 +380,7 @@ static int decode_impl(pcg_plan* p,
     a.scratch_floats = p->scratch_floats;
     a.fmap = fmap;
     a.fcount = fcount;
+    a.llr8 = llr8;
     if (getenv("PCG_OPPROF")) {
         if (!g_prof && hipMalloc(&g_prof, 128 * sizeof(unsigned long long)) == hipSuccess)
             (void)hipMemset(g_prof, 0, 128 * sizeof(unsigned long long));
@@ -352,7 +390,22 @@ static int decode_impl(pcg_plan* p,
         a.flags = (uint32_t)strtoul(fl, nullptr, 0);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc;
-    if (h.L == 1) {
+    if (h.fixed && h.L == 1) {
+        rc = pcg::launch_sc_char(a, s);
+    } else if (h.fixed) {
+        const uint64_t need = pcg::sclc_units(F, h.L, p->wave_lds_floats, llr8 != nullptr);
+        if (p->scratch_floats > 0 && need > p->scratch_frames) {
+            (void)hipFree(p->d_scratch);
+            p->d_scratch = nullptr;
+            p->scratch_frames = 0;
+            hipError_t e = hipMalloc(&p->d_scratch, need * p->scratch_floats * sizeof(uint32_t));
+            if (e != hipSuccess)
+                return hip_fail(e, "hipMalloc(scratch)");
+            p->scratch_frames = need;
+        }
+        a.scratch = p->d_scratch;
+        rc = pcg::launch_scl_char(a, s);
+    } else if (h.L == 1) {
         rc = pcg::launch_sc(a, s);
     } else {
         if (p->scratch_floats > 0) {
@@ -373,6 +426,84 @@ static int decode_impl(pcg_plan* p,
     }
     if (rc != 0)
         return fail(rc, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    return PCG_OK;
+}
+
+int pcg_decode_i8(pcg_plan* p,
+                  const int8_t* llr,
+                  uint64_t F,
+                  uint8_t* info,
+                  uint8_t* ok,
+                  float* metrics,
+                  void* stream)
+{
+    if (!p)
+        return fail(PCG_E_ARG, "null plan");
+    if (!p->host.fixed)
+        return fail(PCG_E_ARG, "int8 LLRs need an 8-bit plan (pcg_plan_create_char)");
+    if (F == 0)
+        return PCG_OK;
+    if (!llr || !info)
+        return fail(PCG_E_ARG, "null llr/info buffer");
+    if (p->device < 0)
+        return fail(PCG_E_NODEVICE, "host-only plan (created with device < 0)");
+    if (F > 0xFFFFFFFFull)
+        return fail(PCG_E_ARG, "at most 2^32 - 1 frames per call");
+    DeviceGuard g(p->device);
+    return decode_impl(p, nullptr, F, info, ok, metrics, stream, nullptr, nullptr, llr);
+}
+
+int pcg_decode_i8_host(pcg_plan* p, const int8_t* llr, uint64_t F, uint8_t* info, uint8_t* ok, float* metrics)
+{
+    if (!p)
+        return fail(PCG_E_ARG, "null plan");
+    if (!p->host.fixed)
+        return fail(PCG_E_ARG, "int8 LLRs need an 8-bit plan (pcg_plan_create_char)");
+    if (F == 0)
+        return PCG_OK;
+    if (!llr || !info)
+        return fail(PCG_E_ARG, "null llr/info buffer");
+    if (p->device < 0)
+        return fail(PCG_E_NODEVICE, "host-only plan (created with device < 0)");
+    DeviceGuard g(p->device);
+    const auto& h = p->host;
+    const uint64_t kb = (h.K + 7) / 8;
+    const uint64_t chunk = std::min<uint64_t>(F, 1u << 16);
+    hipError_t e;
+    if (p->stage_frames < chunk) { // the float staging buffer holds the int8 frames too
+        (void)hipFree(p->d_llr);
+        (void)hipFree(p->d_info);
+        (void)hipFree(p->d_ok);
+        (void)hipFree(p->d_met);
+        p->d_llr = nullptr;
+        p->d_info = nullptr;
+        p->d_ok = nullptr;
+        p->d_met = nullptr;
+        p->stage_frames = 0;
+        if ((e = hipMalloc(&p->d_llr, chunk * h.N * sizeof(float))) != hipSuccess ||
+            (e = hipMalloc(&p->d_info, chunk * std::max<uint64_t>(kb, 1))) != hipSuccess ||
+            (e = hipMalloc(&p->d_ok, chunk)) != hipSuccess ||
+            (e = hipMalloc(&p->d_met, chunk * h.L * sizeof(float))) != hipSuccess)
+            return hip_fail(e, "hipMalloc(staging)");
+        p->stage_frames = chunk;
+    }
+    int8_t* d8 = reinterpret_cast<int8_t*>(p->d_llr);
+    for (uint64_t f0 = 0; f0 < F; f0 += chunk) {
+        const uint64_t n = std::min(chunk, F - f0);
+        if ((e = hipMemcpy(d8, llr + f0 * h.N, n * h.N, hipMemcpyHostToDevice)) != hipSuccess)
+            return hip_fail(e, "hipMemcpy(H2D)");
+        int rc = pcg_decode_i8(p, d8, n, p->d_info, ok ? p->d_ok : nullptr, metrics ? p->d_met : nullptr, nullptr);
+        if (rc != 0)
+            return rc;
+        if ((e = hipMemcpy(info + f0 * kb, p->d_info, n * kb, hipMemcpyDeviceToHost)) != hipSuccess)
+            return hip_fail(e, "hipMemcpy(D2H info)");
+        if (ok && (e = hipMemcpy(ok + f0, p->d_ok, n, hipMemcpyDeviceToHost)) != hipSuccess)
+            return hip_fail(e, "hipMemcpy(D2H ok)");
+        if (metrics &&
+            (e = hipMemcpy(metrics + f0 * h.L, p->d_met, n * h.L * sizeof(float), hipMemcpyDeviceToHost)) !=
+                hipSuccess)
+            return hip_fail(e, "hipMemcpy(D2H metrics)");
+    }
     return PCG_OK;
 }
 

@@ -341,7 +341,18 @@ void Decoder::setSystematic(bool sys) { mSystematic = sys; }
 
 void Decoder::setErrorDetection(ErrorDetection::Detector* pDetector) { mErrorDetector = pDetector; }
 
-void Decoder::setSignal(const float* pLlr) { std::memcpy(mLlr.data(), pLlr, 4 * mBlockLength); }
+void Decoder::setSignal(const float* pLlr)
+{
+    std::memcpy(mLlr.data(), pLlr, 4 * mBlockLength);
+    mSignalI8 = false;
+}
+
+void Decoder::setSignal(const char* pLlr) // FloatContainer::insertLlr(const char*), bitcontainer.cpp:202-207
+{
+    for (size_t i = 0; i < mBlockLength; ++i)
+        mLlr[i] = static_cast<float>(pLlr[i]);
+    mSignalI8 = false;
+}
 
 void Decoder::getDecodedInformationBits(void* pData)
 {
@@ -349,6 +360,18 @@ void Decoder::getDecodedInformationBits(void* pData)
 }
 
 bool Decoder::decode_vector(const float* pLlr, void* pData)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    setSignal(pLlr);
+    const bool r = decode();
+    getDecodedInformationBits(pData);
+    mDecoderDuration = (size_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                           std::chrono::steady_clock::now() - t0)
+                           .count();
+    return r;
+}
+
+bool Decoder::decode_vector(const char* pLlr, void* pData)
 {
     const auto t0 = std::chrono::steady_clock::now();
     setSignal(pLlr);
@@ -391,8 +414,9 @@ void GpuDecoder::initialize(size_t blockLength, const std::vector<unsigned>& fro
     releasePlan();
     // validate (and classify) now so invalid codes fail at construction like the reference
     pcg_plan* probe = nullptr;
-    int rc = pcg_plan_create(&probe, (uint32_t)blockLength, (uint32_t)mListSize, mFrozenBits.data(),
-                             (uint32_t)mFrozenBits.size(), 1, 0, -1);
+    int rc = (mFixed ? pcg_plan_create_char : pcg_plan_create)(&probe, (uint32_t)blockLength, (uint32_t)mListSize,
+                                                                 mFrozenBits.data(), (uint32_t)mFrozenBits.size(),
+                                                                 1, 0, -1);
     if (rc != 0)
         throw_pcg(rc);
     pcg_plan_destroy(probe);
@@ -420,7 +444,7 @@ void GpuDecoder::ensurePlan()
     if (mPlan && kind == mPlanKind && mSystematic == mPlanSys)
         return;
     releasePlan();
-    auto create = mAdaptive ? pcg_plan_create_adaptive : pcg_plan_create;
+    auto create = mAdaptive ? pcg_plan_create_adaptive : (mFixed ? pcg_plan_create_char : pcg_plan_create);
     const int rc = create(&mPlan, (uint32_t)mBlockLength, (uint32_t)mListSize, mFrozenBits.data(),
                           (uint32_t)mFrozenBits.size(), mSystematic ? 1 : 0, kind, mDevice);
     if (rc != 0) {
@@ -431,10 +455,21 @@ void GpuDecoder::ensurePlan()
     mPlanSys = mSystematic;
 }
 
+void GpuDecoder::setSignal(const char* pLlr)
+{
+    if (!mFixed)
+        return Decoder::setSignal(pLlr);
+    mLlr8.assign(pLlr, pLlr + mBlockLength); // CharContainer::insertLlr(const char*): a copy
+    mSignalI8 = true;
+}
+
 bool GpuDecoder::decode()
 {
     uint8_t ok = 0;
-    decodeBatch(mLlr.data(), 1, mOutputContainer.data(), &ok, nullptr);
+    if (mSignalI8)
+        decodeBatchI8(mLlr8.data(), 1, mOutputContainer.data(), &ok, nullptr);
+    else
+        decodeBatch(mLlr.data(), 1, mOutputContainer.data(), &ok, nullptr);
     mLastOk = ok != 0;
     return mLastOk;
 }
@@ -466,6 +501,55 @@ void GpuDecoder::decodeBatchDevice(const float* llr, size_t F, uint8_t* info, ui
         throw_pcg(rc);
 }
 
+bool GpuDecoder::decodeBatchI8(const int8_t* llr, size_t F, uint8_t* info, uint8_t* ok, float* metrics)
+{
+    if (!mFixed) { // float decoders take 8-bit LLRs as floats
+        std::vector<float> f((size_t)F * mBlockLength);
+        for (size_t i = 0; i < f.size(); ++i)
+            f[i] = static_cast<float>(llr[i]);
+        return decodeBatch(f.data(), F, info, ok, metrics);
+    }
+    ensurePlan();
+    std::vector<uint8_t> okv;
+    uint8_t* okp = ok;
+    if (!okp) {
+        okv.assign(F, 0);
+        okp = okv.data();
+    }
+    const int rc = pcg_decode_i8_host(mPlan, llr, F, info, okp, mListSize > 1 ? metrics : nullptr);
+    if (rc != 0)
+        throw_pcg(rc);
+    for (size_t f = 0; f < F; ++f)
+        if (!okp[f])
+            return false;
+    return true;
+}
+
+void GpuDecoder::decodeBatchDeviceI8(const int8_t* llr, size_t F, uint8_t* info, uint8_t* ok, float* metrics,
+                                     void* hipStream)
+{
+    if (!mFixed)
+        throw std::logic_error("int8 device frames need an 8-bit (\"char\") decoder");
+    ensurePlan();
+    const int rc = pcg_decode_i8(mPlan, llr, F, info, ok, mListSize > 1 ? metrics : nullptr, hipStream);
+    if (rc != 0)
+        throw_pcg(rc);
+}
+
+GpuFastSscChar::GpuFastSscChar(size_t blockLength, const std::vector<unsigned>& frozenBits, int device)
+    : GpuDecoder(blockLength, 1, {}, device)
+{
+    mFixed = true;
+    initialize(blockLength, frozenBits);
+}
+
+GpuSclChar::GpuSclChar(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits, int device)
+    : GpuDecoder(blockLength, listSize, {}, device)
+{
+    mFixed = true;
+    initialize(blockLength, frozenBits);
+}
+
 GpuAdaptiveFloat::GpuAdaptiveFloat(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,
                                    int device)
     : GpuDecoder(blockLength, listSize, {}, device)
@@ -477,11 +561,14 @@ GpuAdaptiveFloat::GpuAdaptiveFloat(size_t blockLength, size_t listSize, const st
 Decoder* makeDecoder(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits, int impl)
 {
     Decoder* dec;
-    if (impl != 1 && impl != 2)
-        throw std::logic_error("decoder implementation " + std::to_string(impl) +
-                               " (char / SCAN) is not part of this build (use \"gpu\")");
-    if (listSize <= 1)
+    if (impl == 3)
+        throw std::logic_error("decoder implementation 3 (SCAN) is not part of this build (use \"gpu\")");
+    if (listSize <= 1 && impl == 1)
         dec = new GpuFastSscFloat(blockLength, frozenBits);
+    else if (listSize <= 1)
+        dec = new GpuFastSscChar(blockLength, frozenBits); // decoder.cpp:60-68: default branch
+    else if (impl == 0)
+        dec = new GpuSclChar(blockLength, listSize, frozenBits);
     else if (impl == 2)
         dec = new GpuAdaptiveFloat(blockLength, listSize, frozenBits);
     else
@@ -493,14 +580,22 @@ Decoder* makeDecoder(size_t blockLength, size_t listSize, const std::vector<unsi
 Decoder* create(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits, std::string type)
 {
     std::transform(type.begin(), type.end(), type.begin(), [](unsigned char c) { return std::tolower(c); });
-    // decoder.cpp:35-51: "char" is tested first, then "float", "mixed", "scan"
-    if (type.find("char") != std::string::npos || type.find("scan") != std::string::npos)
-        throw std::logic_error("PolarDecoder type '" + type + "' is not part of this build (use \"gpu\")");
-    if (type.find("gpu") != std::string::npos || type.find("float") != std::string::npos)
-        return makeDecoder(blockLength, listSize, frozenBits, 1);
-    if (type.find("mixed") != std::string::npos)
-        return makeDecoder(blockLength, listSize, frozenBits, 2);
-    throw std::logic_error("Unknown PolarDecoder type!");
+    // decoder.cpp:35-51: "char" is tested first, then "float", "mixed", "scan"; list size < 2
+    // turns every non-char type into the float Fast-SSC decoder
+    int flag;
+    if (type.find("char") != std::string::npos)
+        flag = 0;
+    else if (type.find("gpu") != std::string::npos || type.find("float") != std::string::npos)
+        flag = 1;
+    else if (type.find("mixed") != std::string::npos)
+        flag = 2;
+    else if (type.find("scan") != std::string::npos)
+        flag = 3;
+    else
+        throw std::logic_error("Unknown PolarDecoder type!");
+    if (listSize < 2 && flag != 0)
+        flag = 1;
+    return makeDecoder(blockLength, listSize, frozenBits, flag);
 }
 
 } // namespace Decoding

@@ -31,12 +31,17 @@ struct KernelArgs {
     // (the adaptive decoder's second stage; F bounds *fcount and sizes the grid)
     const uint32_t* fmap;
     const uint32_t* fcount;
+    // 8-bit ("char") plans: F x N int8 channel LLRs; null -> `llr` floats are quantised
+    // in the kernel exactly as CharContainer::insertLlr does
+    const int8_t* llr8;
 };
 
 // LDS floats one SC codeword needs: alpha (N floats, index 0 unused) + packed bits.
 inline uint32_t sc_wave_lds_floats(uint32_t N) { return N + (N >= 64 ? N / 32 : 2) + 2; }
 
 int launch_sc(const KernelArgs& a, hipStream_t stream);
+int launch_sc_char(const KernelArgs& a, hipStream_t stream);   // FastSscFipChar (sc_char_kernel.hip)
+int launch_scl_char(const KernelArgs& a, hipStream_t stream);  // SclFipChar (scl_char_kernel.hip)
 int launch_scl(const KernelArgs& a, hipStream_t stream);
 
 } // namespace pcg
@@ -53,4 +58,8 @@ int sclls_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* ld
                  uint64_t* scratch_floats, uint32_t* virt);
 uint64_t sclls_units(uint64_t F, uint32_t L, uint32_t wave_lds_floats);
 int launch_sclls(const KernelArgs& a, hipStream_t stream);
+// 8-bit SCL (scl_char_kernel.hip): LDS dwords per wave, LDS stage limit, global scratch
+// dwords per wave; persistent waves for a launch of F frames
+int sclc_layout(uint32_t N, uint32_t L, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratch_dwords);
+uint64_t sclc_units(uint64_t F, uint32_t L, uint32_t lds_dwords, bool i8);
 } // namespace pcg

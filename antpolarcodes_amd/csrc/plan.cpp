@@ -177,6 +177,84 @@ void scl_emit(PlanHost& p, const std::vector<uint32_t>& f, uint32_t n, uint32_t 
     p.ops.push_back(mkop(OP_COMB, n, off));
 }
 
+// FastSscFip::createDecoder (fastssc_fip_char.cpp:496-580).  Short (n <= 32) and long
+// variants of RateR / ROne / ZeroR have the same effect on sign bits; the leaves differ.
+void sc_char_emit(PlanHost& p, const std::vector<uint32_t>& f, uint32_t n, uint32_t off)
+{
+    constexpr uint32_t BV = 32; // BYTESPERVECTOR of the AVX2 build
+    const uint32_t nf = (uint32_t)f.size();
+    p.node_count++;
+    auto leaf = [&](uint32_t code) {
+        p.node_types.push_back((int)code);
+        p.ops.push_back(mkop(code, n, off));
+    };
+    if (nf == n) return leaf(OP_C_R0);
+    if (nf == 0) return leaf(OP_C_R1);
+    if (nf == n - 1) return leaf(n <= BV ? OP_C_REPS : OP_C_REP);
+    if (nf == 1) return leaf(n <= BV ? OP_C_SPCS : OP_C_SPC);
+    if (nf == n - 2 && n >= BV) return leaf(OP_C_DREP);
+    const uint32_t h = n / 2;
+    std::vector<uint32_t> lf, rf;
+    split(f, h, lf, rf);
+    if (n <= BV) {
+        if (lf.size() == h && rf.empty()) return leaf(OP_C_ZONES);
+        if (lf.size() == h && rf.size() == 1) return leaf(OP_C_ZSPCS);
+    } else if (lf.size() == h && rf.size() == 1) {
+        return leaf(OP_C_ZSPC);
+    }
+    p.node_types.push_back(0);
+    // (Short)ROneNode / (Short)ZeroRNode construct both children (RateRNode's constructor,
+    // fastssc_fip_char.cpp:81-94) but decode only one: count the other, emit nothing
+    auto count_only = [&](const std::vector<uint32_t>& cf) {
+        PlanHost tmp;
+        sc_char_emit(tmp, cf, h, 0);
+        p.node_count += tmp.node_count;
+    };
+    if (rf.empty()) { // (Short)ROneNode
+        p.ops.push_back(mkop(OP_F, n, off));
+        sc_char_emit(p, lf, h, off);
+        count_only(rf);
+        p.ops.push_back(mkop(OP_RONE, n, off));
+        return;
+    }
+    if (lf.size() == h) { // (Short)ZeroRNode
+        count_only(lf);
+        p.ops.push_back(mkop(OP_G0, n, off));
+        sc_char_emit(p, rf, h, off + h);
+        p.ops.push_back(mkop(OP_COPY0, n, off));
+        return;
+    }
+    p.ops.push_back(mkop(OP_F, n, off)); // (Short)RateRNode
+    sc_char_emit(p, lf, h, off);
+    p.ops.push_back(mkop(OP_G, n, off));
+    sc_char_emit(p, rf, h, off + h);
+    p.ops.push_back(mkop(OP_COMB, n, off));
+}
+
+// SclFip::createDecoder (scl_fip_char.cpp:729-752); RateRNode::decode order (:315-349).
+void scl_char_emit(PlanHost& p, const std::vector<uint32_t>& f, uint32_t n, uint32_t off)
+{
+    const uint32_t nf = (uint32_t)f.size();
+    p.node_count++;
+    auto leaf = [&](uint32_t code) {
+        p.node_types.push_back((int)code);
+        p.ops.push_back(mkop(code, n, off));
+    };
+    if (nf == n) return leaf(OP_CS_R0);
+    if (nf == 0) return leaf(OP_CS_R1);
+    if (nf == n - 1) return leaf(OP_CS_REP);
+    if (nf == 1) return leaf(OP_CS_SPC);
+    const uint32_t h = n / 2;
+    std::vector<uint32_t> lf, rf;
+    split(f, h, lf, rf);
+    p.node_types.push_back(0);
+    p.ops.push_back(mkop(OP_F, n, off));
+    scl_char_emit(p, lf, h, off);
+    p.ops.push_back(mkop(OP_G, n, off));
+    scl_char_emit(p, rf, h, off + h);
+    p.ops.push_back(mkop(OP_COMB, n, off));
+}
+
 } // namespace
 
 int build_plan(PlanHost& p,
@@ -186,7 +264,8 @@ int build_plan(PlanHost& p,
                uint32_t nf,
                int systematic,
                int crc_kind,
-               std::string* err)
+               std::string* err,
+               int fixed)
 {
     p = PlanHost();
     if (N < 8 || N > 32768 || (N & (N - 1))) {
@@ -218,6 +297,7 @@ int build_plan(PlanHost& p,
     p.systematic = systematic ? 1 : 0;
     p.crc_kind = crc_kind;
     p.frozen.assign(frozen, frozen + nf);
+    p.fixed = fixed ? 1 : 0;
     // SCL kernel choice (dev switch PCG_SCL_KERNEL=wave selects the cooperative
     // one-codeword-per-wave kernel); the lane-serial kernel always runs size-8
     // subtrees in registers, the cooperative one only for L <= 8 (<= 64 candidates)
@@ -227,7 +307,11 @@ int build_plan(PlanHost& p,
     }
     p.scl_st8 = p.scl_kind == 0 || (L <= 8 && getenv("PCG_SCL_NO_ST8") == nullptr);
     try {
-        if (L == 1)
+        if (p.fixed && L == 1)
+            sc_char_emit(p, p.frozen, N, 0);
+        else if (p.fixed)
+            scl_char_emit(p, p.frozen, N, 0);
+        else if (L == 1)
             sc_emit(p, p.frozen, N, 0);
         else
             scl_emit(p, p.frozen, N, 0);

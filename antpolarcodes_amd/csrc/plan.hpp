@@ -49,6 +49,24 @@ enum OpCode : uint32_t {
     // A whole size-8 SCL subtree run lane-serially (lane = path) in registers; the
     // next schedule word is its descriptor (see scl_emit in plan.cpp).
     OP_S_ST8 = 44,
+    // 8-bit fixed-point Fast-SSC leaves (FastSscFipChar, fastssc_fip_char.cpp); the
+    // internal ops above (F, G, G0, RONE, COMB, COPY0) take the char semantics of
+    // fip_char.h in the int8 kernels
+    OP_C_R0 = 64,    // RateZeroDecoder            :202-208
+    OP_C_R1 = 65,    // RateOneDecoder             :210-215
+    OP_C_REP = 66,   // RepetitionDecoder, n > 32  :225-241
+    OP_C_REPS = 67,  // ShortRepetitionDecoder     :265-272
+    OP_C_DREP = 68,  // DoubleRepetitionDecoder    :249-263
+    OP_C_SPC = 69,   // SpcDecoder, n > 32         :274-303
+    OP_C_SPCS = 70,  // ShortSpcDecoder            :305-319
+    OP_C_ZSPC = 71,  // ZeroSpcDecoder, n > 32     :321-359
+    OP_C_ZSPCS = 72, // ShortZeroSpcDecoder        :361-388
+    OP_C_ZONES = 73, // ShortZeroOneDecoder        :390-399
+    // 8-bit fixed-point SCL leaves (SclFipChar, scl_fip_char.cpp)
+    OP_CS_R0 = 80,  // RateZeroDecoder   :387-421
+    OP_CS_R1 = 81,  // RateOneDecoder    :423-505
+    OP_CS_REP = 82, // RepetitionDecoder :508-580
+    OP_CS_SPC = 83, // SpcDecoder        :583-726
 };
 
 // ST8 descriptor: per size-4 child c (c = 0 left, 1 right) at bits 8c..8c+6:
@@ -74,6 +92,7 @@ struct PlanHost {
     std::vector<int> node_types;    // pre-order census (op code of each node; 0 = internal)
     bool scl_st8 = true;            // emit lane-serial size-8 subtrees for SCL
     int scl_kind = 0;               // SCL kernel: 0 lane-serial (sclls_kernel.hip), 1 one codeword per wave
+    int fixed = 0;                  // 1: the reference's 8-bit decoders (FastSscFipChar / SclFipChar)
 };
 
 // Returns 0, or a negative pcg.h error code with *err set.
@@ -84,6 +103,7 @@ int build_plan(PlanHost& p,
                uint32_t nf,
                int systematic,
                int crc_kind,
-               std::string* err);
+               std::string* err,
+               int fixed = 0);
 
 } // namespace pcg

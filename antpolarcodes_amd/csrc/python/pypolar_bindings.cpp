@@ -4,6 +4,7 @@
 // plus PolarDecoder.decode_batch / decode_device for batched GPU decoding.
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#include <type_traits>
 #include <pybind11/stl.h>
 
 #include <polarcode/construction/constructor.h>
@@ -35,6 +36,41 @@ struct PyEncoder {
 using f32array = py::array_t<float, py::array::c_style | py::array::forcecast>;
 using u8array = py::array_t<uint8_t, py::array::c_style | py::array::forcecast>;
 using f64array = py::array_t<double, py::array::c_style | py::array::forcecast>;
+using i8array = py::array_t<int8_t, py::array::c_style | py::array::forcecast>;
+
+// decode_batch over float32 or int8 frames (F x N): info [, ok] [, metrics]
+template <typename T>
+py::object decode_batch_impl(PyDecoder& s, const py::array_t<T, py::array::c_style | py::array::forcecast>& a,
+                             bool return_ok, bool return_metrics)
+{
+    py::buffer_info in = a.request();
+    const size_t N = s.dec->blockLength(), L = s.dec->getListSize();
+    if (in.ndim != 2 || (size_t)in.shape[1] != N)
+        throw std::runtime_error("decode_batch expects a (frames, blockLength) float32 or int8 array");
+    const size_t F = (size_t)in.shape[0], kb = (s.dec->infoLength() + 7) / 8;
+    py::array_t<uint8_t> info({ F, kb });
+    py::array_t<uint8_t> ok(F);
+    py::array_t<float> met({ F, L });
+    {
+        py::gil_scoped_release nogil;
+        if constexpr (std::is_same<T, float>::value)
+            s.dec->decodeBatch(static_cast<const float*>(in.ptr), F, info.mutable_data(), ok.mutable_data(),
+                               return_metrics ? met.mutable_data() : nullptr);
+        else
+            s.dec->decodeBatchI8(static_cast<const int8_t*>(in.ptr), F, info.mutable_data(), ok.mutable_data(),
+                                 return_metrics ? met.mutable_data() : nullptr);
+    }
+    if (!return_ok && !return_metrics)
+        return std::move(info);
+    py::tuple t(1 + (return_ok ? 1 : 0) + (return_metrics ? 1 : 0));
+    size_t k = 0;
+    t[k++] = info;
+    if (return_ok)
+        t[k++] = ok;
+    if (return_metrics)
+        t[k++] = met;
+    return std::move(t);
+}
 
 // Puncturer.puncture / depuncture for one element type (puncturer_python.cc:37-160)
 template <typename T>
@@ -109,34 +145,49 @@ PYBIND11_MODULE(_pypolar, m)
                  std::memcpy(res.request().ptr, tmp.data(), s.dec->infoLength() / 8);
                  return res;
              })
+        .def("decode_vector", // the reference's int8 overload (decoder_python.cc:58-74)
+             [](PyDecoder& s, const i8array& a) {
+                 py::buffer_info in = a.request();
+                 if (in.ndim != 1)
+                     throw std::runtime_error("Only ONE-dimensional vectors allowed!");
+                 if ((size_t)in.size != s.dec->blockLength())
+                     throw std::runtime_error("Input vector size != blockSize // 8!");
+                 auto res = py::array_t<uint8_t>(s.dec->infoLength() / 8);
+                 std::vector<uint8_t> tmp(s.dec->infoLength() / 8 + 8);
+                 s.dec->decode_vector(static_cast<const char*>(in.ptr), tmp.data());
+                 std::memcpy(res.request().ptr, tmp.data(), s.dec->infoLength() / 8);
+                 return res;
+             })
         .def(
             "decode_batch",
-            [](PyDecoder& s, const f32array& a, bool return_ok, bool return_metrics) -> py::object {
-                py::buffer_info in = a.request();
-                const size_t N = s.dec->blockLength(), L = s.dec->getListSize();
-                if (in.ndim != 2 || (size_t)in.shape[1] != N)
-                    throw std::runtime_error("decode_batch expects a (frames, blockLength) float32 array");
-                const size_t F = (size_t)in.shape[0], kb = (s.dec->infoLength() + 7) / 8;
-                py::array_t<uint8_t> info({ F, kb });
-                py::array_t<uint8_t> ok(F);
-                py::array_t<float> met({ F, L });
-                {
-                    py::gil_scoped_release nogil;
-                    s.dec->decodeBatch(static_cast<const float*>(in.ptr), F, info.mutable_data(),
-                                       ok.mutable_data(), return_metrics ? met.mutable_data() : nullptr);
-                }
-                if (!return_ok && !return_metrics)
-                    return std::move(info);
-                py::tuple t(1 + (return_ok ? 1 : 0) + (return_metrics ? 1 : 0));
-                size_t k = 0;
-                t[k++] = info;
-                if (return_ok)
-                    t[k++] = ok;
-                if (return_metrics)
-                    t[k++] = met;
-                return std::move(t);
+            [](PyDecoder& s, const f32array& a, bool return_ok, bool return_metrics) {
+                return decode_batch_impl<float>(s, a, return_ok, return_metrics);
             },
             py::arg("llrs"), py::arg("return_ok") = false, py::arg("return_metrics") = false)
+        .def(
+            "decode_batch",
+            [](PyDecoder& s, const i8array& a, bool return_ok, bool return_metrics) {
+                return decode_batch_impl<int8_t>(s, a, return_ok, return_metrics);
+            },
+            py::arg("llrs"), py::arg("return_ok") = false, py::arg("return_metrics") = false)
+        .def("isFixedPoint",
+             [](PyDecoder& s) {
+                 auto* g = dynamic_cast<Decoding::GpuDecoder*>(s.dec.get());
+                 return g != nullptr && g->isFixedPoint();
+             })
+        .def(
+            "decode_device_i8",
+            [](PyDecoder& s, uintptr_t llr, size_t F, uintptr_t info, uintptr_t ok, uintptr_t metrics,
+               uintptr_t stream) {
+                auto* g = dynamic_cast<Decoding::GpuDecoder*>(s.dec.get());
+                if (!g)
+                    throw std::logic_error("not a GPU decoder");
+                g->decodeBatchDeviceI8(reinterpret_cast<const int8_t*>(llr), F, reinterpret_cast<uint8_t*>(info),
+                                       reinterpret_cast<uint8_t*>(ok), reinterpret_cast<float*>(metrics),
+                                       reinterpret_cast<void*>(stream));
+            },
+            py::arg("llr_ptr"), py::arg("frames"), py::arg("info_ptr"), py::arg("ok_ptr") = 0,
+            py::arg("metrics_ptr") = 0, py::arg("stream") = 0)
         .def(
             "decode_device",
             [](PyDecoder& s, uintptr_t llr, size_t F, uintptr_t info, uintptr_t ok, uintptr_t metrics,

@@ -1,0 +1,748 @@
+// scl_char_kernel.hip -- lane-serial batched 8-bit fixed-point CRC-aided SCL decoding
+// (the reference's SclFipChar, src/polarcode/decoding/scl_fip_char.cpp) on CDNA4.
+//
+// Lane = one path of one codeword; a wave decodes G = 64 / LP codewords (LP = L
+// rounded up to a power of two), lanes g*LP .. g*LP+LP-1 holding codeword g's paths.
+// Every codeword shares the plan's schedule and the path count after each leaf only
+// depends on the schedule, so the wave walks the schedule uniformly while each lane
+// runs the reference's per-path loops serially over its own LLR bytes.
+//
+// Path state of lane l = g*LP + p:
+//   * metric (int32; the reference's `long` metrics are exact integers bounded by
+//     128 N per frame, and every frame starts from 0 -- see DESIGN.md Q8);
+//   * LLR bytes of stages s < top-1, packed 4 per dword, dword c of lane l's column at
+//     [(c * 64) + l] of the stage region (LDS for s < Sl, a per-wave global slab for
+//     Sl <= s < top-1), addressed through a 5-bit-per-stage slot table (the lane that
+//     holds this path's stage s): an F/G rewrites every path's stage s-1 in its own
+//     lane, a branching leaf copies the table of the path a survivor descends from --
+//     the reference's lazy DataPool copy (scl_fip_char.cpp:21-171) without moving LLRs;
+//   * stage top-1 (the root's children) is never stored: its bytes are recomputed from
+//     the channel (F for the left child, G with the path's own left-half bits for the
+//     right child) wherever they are read;
+//   * the packed codeword sign bits, one LDS word column per lane.
+// Leaves follow scl_fip_char.cpp literally on the bytes: Rate-0 penalty, Rate-1 / SPC
+// weakest-LLR search (findWeakLlrs' swap-selection reproduced exactly from a one-pass
+// candidate set: the first `passes` positions plus the `passes` smallest (value, index)
+// pairs of the rest are the only elements the selection can touch), Repetition, and the
+// list pruning (simplePartialSortDescending over int metrics, where ties are the rule,
+// not the exception) simulated literally in LDS with a group-parallel argmax per pass.
+#include "kernels.hpp"
+#include "plan.hpp"
+#include "wave.hpp"
+
+#include <stdio.h>
+#include <stdlib.h>
+
+namespace pcg {
+
+namespace {
+
+constexpr int INT_NEG = -2147483647 - 1;
+
+PCG_DEV int sat8(int v) { return v < -128 ? -128 : (v > 127 ? 127 : v); }
+PCG_DEV int sbyte(uint32_t d, uint32_t b) { return (int)(int8_t)(uint8_t)(d >> (8 * b)); }
+PCG_DEV uint32_t ubyte(int v, uint32_t b) { return ((uint32_t)v & 0xffu) << (8 * b); }
+
+// FastSscFip::F_function_calc / G_function_calc (fip_char.h:35-64)
+PCG_DEV int fip_f(int l, int r)
+{
+    const bool neg = (l ^ r) < 0;
+    int a = l > -127 ? l : -127, b = r > -127 ? r : -127;
+    a = a < 0 ? -a : a;
+    b = b < 0 ? -b : b;
+    a = a > 1 ? a : 1;
+    b = b > 1 ? b : 1;
+    const int m = a < b ? a : b;
+    return neg ? -m : m;
+}
+PCG_DEV int fip_g(int l, int r, uint32_t bit) { return sat8(bit ? r - l : r + l); }
+
+PCG_DEV uint32_t f4(uint32_t a, uint32_t b)
+{
+    uint32_t o = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+        o |= ubyte(fip_f(sbyte(a, k), sbyte(b, k)), k);
+    return o;
+}
+PCG_DEV uint32_t g4(uint32_t a, uint32_t b, uint32_t nib)
+{
+    uint32_t o = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k)
+        o |= ubyte(fip_g(sbyte(a, k), sbyte(b, k), (nib >> k) & 1u), k);
+    return o;
+}
+// sign bits of 4 bytes as a nibble
+PCG_DEV uint32_t sign4(uint32_t d)
+{
+    return ((d >> 7) & 1u) | ((d >> 14) & 2u) | ((d >> 21) & 4u) | ((d >> 28) & 8u);
+}
+
+// stage regions in dwords per lane: stage t has max(1, 2^t / 4) dwords
+__host__ __device__ inline uint32_t st_units(uint32_t s) { return s <= 2 ? s : (1u << (s - 2)) + 1u; }
+
+struct Layout {
+    uint32_t Sl;       // stages < Sl in LDS
+    uint32_t mt;       // first recomputed stage (top-1), stages [Sl, mt) in global scratch
+    uint32_t bits;     // LDS dword offset of the bit rows (64 x W)
+    uint32_t cand;     // LDS dword offset of the candidate lists (2 x 512)
+    uint32_t lds;      // LDS dwords per wave
+    uint64_t gdwords;  // global scratch dwords per wave
+};
+
+__host__ __device__ inline Layout make_layout(uint32_t N, uint32_t Sl)
+{
+    Layout y;
+    const uint32_t top = (uint32_t)__builtin_ctz(N);
+    y.mt = top - 1;
+    y.Sl = Sl < y.mt ? Sl : y.mt;
+    y.bits = 64u * st_units(y.Sl);
+    const uint32_t W = N >= 32 ? N / 32 : 1u;
+    y.cand = y.bits + 64u * W;
+    y.lds = y.cand + 1024u;
+    y.gdwords = 64ull * (st_units(y.mt) - st_units(y.Sl));
+    return y;
+}
+
+template <int LP, bool I8>
+struct Wave {
+    uint32_t* lds;
+    uint32_t* gs;
+    const void* chan; // this lane's frame: int8 or float
+    uint32_t N, top, L;
+    Layout ly;
+    uint32_t lane, p, gb;
+    uint64_t ptr = 0;   // slot of stage s at bits 5s
+    int m = 0;          // path metric
+    bool right = false; // root's right child active (recomputed stage top-1 = G)
+
+    PCG_DEV uint32_t* row() const { return lds + ly.bits + lane; } // word w at [w * 64]
+    PCG_DEV uint32_t slot(uint32_t s) const { return gb | (uint32_t)((ptr >> (5u * s)) & 31u); }
+    PCG_DEV void own(uint32_t s)
+    {
+        const uint32_t sh = 5u * s;
+        ptr = (ptr & ~(31ull << sh)) | ((uint64_t)p << sh);
+    }
+
+    // dword c of the channel frame, quantised (CharContainer::insertLlr) for float input
+    PCG_DEV uint32_t chan_dw(uint32_t c) const
+    {
+        if constexpr (I8) {
+            return reinterpret_cast<const uint32_t*>(chan)[c];
+        } else {
+            const float4 v = reinterpret_cast<const float4*>(chan)[c];
+            const float x[4] = { v.x, v.y, v.z, v.w };
+            uint32_t o = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) {
+                int q;
+                if (N >= 32) { // convert_f32_to_int8_large: cvtps_epi32 + saturating packs
+                    if (!(x[k] < 2147483648.0f) || x[k] < -2147483648.0f) {
+                        q = -128;
+                    } else {
+                        const float r = __builtin_rintf(x[k]);
+                        q = r <= -128.0f ? -128 : (r >= 127.0f ? 127 : (int)r);
+                    }
+                } else { // vectorizedFtoC
+                    float t = x[k] > -128.0f ? x[k] : -128.0f;
+                    t = t < 127.0f ? t : 127.0f;
+                    q = (int)__builtin_rintf(t);
+                }
+                o |= ubyte(q, k);
+            }
+            return o;
+        }
+    }
+    // dword c of stage s of this path (any stage <= top)
+    PCG_DEV uint32_t ld(uint32_t s, uint32_t c) const
+    {
+        if (s == top)
+            return chan_dw(c);
+        if (s == ly.mt) { // recomputed root child
+            const uint32_t a = chan_dw(c), b = chan_dw(c + (N >> 3));
+            if (!right)
+                return f4(a, b);
+            const uint32_t w = row()[((4u * c) >> 5) << 6];
+            return g4(a, b, (w >> ((4u * c) & 31u)) & 0xfu);
+        }
+        const uint32_t l = slot(s);
+        if (s < ly.Sl)
+            return lds[64u * st_units(s) + (c << 6) + l];
+        return gs[64ull * (st_units(s) - st_units(ly.Sl)) + ((uint64_t)c << 6) + l];
+    }
+    // small stages: the whole stage in one dword
+    PCG_DEV void st(uint32_t s, uint32_t c, uint32_t v)
+    {
+        if (s < ly.Sl)
+            lds[64u * st_units(s) + (c << 6) + lane] = v;
+        else
+            gs[64ull * (st_units(s) - st_units(ly.Sl)) + ((uint64_t)c << 6) + lane] = v;
+    }
+    // packed bits [o, o+c) of the own row, c <= 32 and inside one word
+    PCG_DEV uint32_t bits_at(uint32_t o, uint32_t c) const
+    {
+        const uint32_t w = row()[(o >> 5) << 6];
+        return c >= 32 ? w : (w >> (o & 31u)) & ((1u << c) - 1u);
+    }
+    PCG_DEV void put_row(uint32_t o, uint32_t c, uint32_t v)
+    {
+        uint32_t* r = row() + ((o >> 5) << 6);
+        if (c >= 32) {
+            *r = v;
+        } else {
+            const uint32_t sh = o & 31u, msk = ((1u << c) - 1u) << sh;
+            *r = (*r & ~msk) | ((v << sh) & msk);
+        }
+    }
+};
+
+// F / G of the node at stage s (n = 2^s) into stage s-1 of the own lane
+template <int LP, bool I8>
+PCG_DEV void op_fg(Wave<LP, I8>& w, bool g, uint32_t s, uint32_t o, bool act)
+{
+    const uint32_t cs = s - 1, h = 1u << cs;
+    if (s == w.top) { // the root's children are recomputed, never stored
+        w.right = g;
+        return;
+    }
+    if (act) {
+        if (h >= 4) {
+            const uint32_t hq = h >> 2;
+            for (uint32_t c = 0; c < hq; ++c) {
+                const uint32_t a = w.ld(s, c), b = w.ld(s, c + hq);
+                const uint32_t v = g ? g4(a, b, w.bits_at(o + 4u * c, 4)) : f4(a, b);
+                w.st(cs, c, v);
+            }
+        } else { // h = 1, 2: stage s is 2h bytes of one dword
+            const uint32_t d = w.ld(s, 0);
+            const uint32_t nib = g ? w.bits_at(o, h) : 0u;
+            uint32_t v = 0;
+            for (uint32_t k = 0; k < h; ++k) {
+                const int l = sbyte(d, k), r = sbyte(d, k + h);
+                v |= ubyte(g ? fip_g(l, r, (nib >> k) & 1u) : fip_f(l, r), k);
+            }
+            w.st(cs, 0, v);
+        }
+    }
+    w.own(cs);
+}
+
+// CombineBits (fip_char.h:165-201) on sign bits: bit[o+i] ^= bit[o+h+i]
+template <int LP, bool I8>
+PCG_DEV void op_comb(Wave<LP, I8>& w, uint32_t s, uint32_t o, bool act)
+{
+    if (!act)
+        return;
+    const uint32_t h = 1u << (s - 1);
+    uint32_t* r = w.row();
+    if (h >= 32) {
+        for (uint32_t k = 0; k < h / 32; ++k)
+            r[((o >> 5) + k) << 6] ^= r[(((o + h) >> 5) + k) << 6];
+    } else {
+        const uint32_t sh = o & 31u, msk = ((1u << h) - 1u) << sh;
+        const uint32_t x = r[(o >> 5) << 6];
+        r[(o >> 5) << 6] = x ^ ((x >> h) & msk);
+    }
+}
+
+// findWeakLlrs(idx, T, n, KW) (arrayfuncs.h:209-231) with T = |max(llr, -127)|: the
+// swap-selection's results (T[0..KW), idx[0..KW)) from one streaming pass.  Only the
+// first `lim` positions (they get displaced) and the lim smallest (value, index) pairs of
+// the remaining positions can be selected, so the literal selection runs on <= 2 lim
+// elements with their positions.
+template <int KW, int LP, bool I8>
+PCG_DEV void weak_llrs(const Wave<LP, I8>& w, uint32_t s, uint32_t n, int (&T)[KW], uint32_t (&I)[KW],
+                       uint32_t& par)
+{
+    const uint32_t lim = n - 1 < (uint32_t)KW ? n - 1 : (uint32_t)KW;
+    int v0[KW], sv[KW];
+    uint32_t si[KW];
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+        v0[k] = 0x7fffffff;
+        sv[k] = 0x7fffffff;
+        si[k] = 0xffffffffu;
+    }
+    par = 0;
+    const uint32_t nd = n >= 4 ? n >> 2 : 1u;
+    for (uint32_t c = 0; c < nd; ++c) {
+        const uint32_t d = w.ld(s, c);
+#pragma unroll
+        for (uint32_t b = 0; b < 4; ++b) {
+            const uint32_t i = 4u * c + b;
+            if (i < n) {
+                const int l = sbyte(d, b);
+                par ^= l < 0 ? 1u : 0u;
+                int t = l > -127 ? l : -127;
+                t = t < 0 ? -t : t;
+                if (i < lim) {
+#pragma unroll
+                    for (int k = 0; k < KW; ++k)
+                        if ((uint32_t)k == i)
+                            v0[k] = t;
+                } else if (t < sv[KW - 1]) { // stable insertion into the sorted set
+#pragma unroll
+                    for (int k = KW - 1; k >= 0; --k) {
+                        const bool shift = k > 0 && t < sv[k > 0 ? k - 1 : 0];
+                        if (t < sv[k]) {
+                            if (shift) {
+                                sv[k] = sv[k - 1];
+                                si[k] = si[k - 1];
+                            } else {
+                                sv[k] = t;
+                                si[k] = i;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+    }
+    // literal swap-selection on the candidate elements: e < KW: position e (value v0),
+    // e >= KW: the sorted set (position = index si)
+    int ev[2 * KW];
+    uint32_t ep[2 * KW], ei[2 * KW];
+#pragma unroll
+    for (int e = 0; e < KW; ++e) {
+        ev[e] = v0[e];
+        ep[e] = (uint32_t)e < lim ? (uint32_t)e : 0xffffffffu;
+        ei[e] = (uint32_t)e;
+        ev[KW + e] = sv[e];
+        ep[KW + e] = si[e];
+        ei[KW + e] = si[e];
+    }
+#pragma unroll
+    for (int i = 0; i < KW; ++i) {
+        if ((uint32_t)i < lim) {
+            int bv = 0x7fffffff, bw = 0;
+            uint32_t bp = 0xffffffffu;
+#pragma unroll
+            for (int e = 0; e < 2 * KW; ++e)
+                if (ep[e] != 0xffffffffu && ep[e] >= (uint32_t)i && (ev[e] < bv || (ev[e] == bv && ep[e] < bp))) {
+                    bv = ev[e];
+                    bp = ep[e];
+                    bw = e;
+                }
+#pragma unroll
+            for (int e = 0; e < 2 * KW; ++e)
+                if (ep[e] == (uint32_t)i)
+                    ep[e] = bp;
+#pragma unroll
+            for (int e = 0; e < 2 * KW; ++e)
+                if (e == bw)
+                    ep[e] = (uint32_t)i;
+            T[i] = bv;
+            I[i] = ei[bw];
+        } else { // after lim = n-1 passes position i holds the remaining element
+            T[i] = 127;
+            I[i] = (uint32_t)i;
+#pragma unroll
+            for (int e = 0; e < 2 * KW; ++e)
+                if (ep[e] == (uint32_t)i) {
+                    T[i] = ev[e];
+                    I[i] = ei[e];
+                }
+        }
+    }
+}
+
+// flip masks over (I0..I3) per candidate (scl_fip_char.cpp:451-466, 640-690)
+__constant__ uint8_t kFlipR1[4] = { 0x0, 0x1, 0x2, 0x3 };
+__constant__ uint8_t kFlipSpcOdd[8] = { 0x1, 0x2, 0x4, 0x8, 0x7, 0xB, 0xD, 0xE };
+__constant__ uint8_t kFlipSpcEven[8] = { 0x0, 0x3, 0x5, 0x9, 0x6, 0xA, 0xC, 0xF };
+
+template <int LP>
+PCG_DEV void grp_argmax_i(int& v, uint32_t& q)
+{
+#pragma unroll
+    for (int d = 1; d < LP; d <<= 1) {
+        const int ov = __shfl_xor(v, d, 64);
+        const uint32_t oq = __shfl_xor(q, d, 64);
+        if (ov > v || (ov == v && oq < q)) {
+            v = ov;
+            q = oq;
+        }
+    }
+}
+
+enum { LK_R1 = 0, LK_REP = 1, LK_SPC = 2 };
+
+// A branching leaf: candidates, pruning, survivors' state (RateOneDecoder :423-505,
+// RepetitionDecoder :508-580, SpcDecoder :583-726)
+template <int LP, bool I8>
+PCG_DEV void op_branch(Wave<LP, I8>& w, uint32_t kind, uint32_t s, uint32_t o, uint32_t& P, bool frame_ok)
+{
+    const uint32_t n = 1u << s;
+    const uint32_t k = kind == LK_R1 ? 4u : (kind == LK_REP ? 2u : 8u);
+    const uint32_t lk = kind == LK_R1 ? 2u : (kind == LK_REP ? 1u : 3u);
+    const bool act = w.p < P;
+    int* V = reinterpret_cast<int*>(w.lds + w.ly.cand) + (w.gb / LP) * (8 * LP);
+    uint32_t* ID = w.lds + w.ly.cand + 512u + (w.gb / LP) * (8 * LP);
+    int T[4] = { 0, 0, 0, 0 };
+    uint32_t I[4] = { 0, 0, 0, 0 }, par = 0;
+    if (act) {
+        int c[8];
+        const int m = w.m;
+        if (kind == LK_REP) {
+            int z = 0, on = 0;
+            const uint32_t nd = n >= 4 ? n >> 2 : 1u;
+            for (uint32_t cc = 0; cc < nd; ++cc) {
+                const uint32_t d = w.ld(s, cc);
+                for (uint32_t b = 0; b < 4; ++b)
+                    if (4u * cc + b < n) {
+                        const int l = sbyte(d, b);
+                        z += l < 0 ? l : 0;
+                        on += l > 0 ? l : 0;
+                    }
+            }
+            c[0] = m + z;
+            c[1] = m - on;
+        } else if (kind == LK_R1) {
+            int t2[2];
+            uint32_t i2[2];
+            weak_llrs<2>(w, s, n, t2, i2, par);
+            T[0] = t2[0];
+            T[1] = t2[1];
+            I[0] = i2[0];
+            I[1] = i2[1];
+            c[0] = m;
+            c[1] = m - T[0];
+            c[2] = m - T[1];
+            c[3] = m - T[0] - T[1];
+        } else {
+            weak_llrs<4>(w, s, n, T, I, par);
+            int mm = m, wk = 0;
+            if (par) // odd parity (scl_fip_char.cpp:640-653)
+                mm -= T[0];
+            else
+                wk = T[0];
+            c[0] = mm;
+            c[1] = mm - wk - T[1];
+            c[2] = mm - wk - T[2];
+            c[3] = mm - wk - T[3];
+            c[4] = mm - T[1] - T[2];
+            c[5] = mm - T[1] - T[3];
+            c[6] = mm - T[2] - T[3];
+            c[7] = mm - wk - T[1] - T[2] - T[3];
+        }
+        for (uint32_t j = 0; j < k; ++j) {
+            V[w.p * k + j] = c[j];
+            ID[w.p * k + j] = w.p * k + j;
+        }
+    }
+    wsync();
+    // simplePartialSortDescending(idx, metrics, np, size) (arrayfuncs.h:161-183)
+    const uint32_t size = k * P, np = size < w.L ? size : w.L;
+    const uint32_t lim = size - 1 < np ? size - 1 : np;
+    for (uint32_t i = 0; i < lim; ++i) {
+        int bv = INT_NEG;
+        uint32_t bq = 0xffffffffu;
+        for (uint32_t q = i + w.p; q < size; q += LP) {
+            const int v = V[q];
+            if (bq == 0xffffffffu || v > bv) {
+                bv = v;
+                bq = q;
+            }
+        }
+        grp_argmax_i<LP>(bv, bq);
+        if (w.p == 0 && bq != i) {
+            const int tv = V[i];
+            const uint32_t ti = ID[i];
+            V[i] = V[bq];
+            ID[i] = ID[bq];
+            V[bq] = tv;
+            ID[bq] = ti;
+        }
+        wsync();
+    }
+    // survivors
+    const bool surv = w.p < np;
+    const uint32_t id = surv ? ID[w.p] : 0u;
+    const int nm = surv ? V[w.p] : 0;
+    wsync();
+    const uint32_t src = id >> lk, j = id & (k - 1u);
+    const uint32_t sl = w.gb | src;
+    const uint64_t nptr = __shfl(w.ptr, (int)sl, 64);
+    const uint32_t spar = __shfl(par, (int)sl, 64);
+    uint32_t sI[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        sI[q] = __shfl(I[q], (int)sl, 64);
+    // codeword prefix [0, o) from the source path (read all, then write)
+    const uint32_t W = w.N >= 32 ? w.N / 32 : 1u;
+    const uint32_t pw = (o + 31u) >> 5;
+    uint32_t* rowb = w.lds + w.ly.bits;
+    for (uint32_t b0 = 0; b0 < pw; b0 += 8) {
+        uint32_t t[8];
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q)
+            t[q] = (b0 + q < pw && b0 + q < W) ? rowb[((b0 + q) << 6) + sl] : 0u;
+        wsync();
+        if (surv && src != w.p)
+#pragma unroll
+            for (uint32_t q = 0; q < 8; ++q)
+                if (b0 + q < pw && b0 + q < W)
+                    rowb[((b0 + q) << 6) + w.lane] = t[q];
+        wsync();
+    }
+    if (surv) {
+        w.ptr = nptr;
+        w.m = nm;
+        // leaf bits: hard decisions of the source path's stage-s bytes with the
+        // candidate's flips (NextBit = NextLlr, then ~ at the hinted indices)
+        if (kind == LK_REP) {
+            const uint32_t v = j ? 0xffffffffu : 0u;
+            if (n >= 32)
+                for (uint32_t q = 0; q < n / 32; ++q)
+                    w.row()[((o >> 5) + q) << 6] = v;
+            else
+                w.put_row(o, n, v);
+        } else {
+            const uint32_t fm = kind == LK_R1 ? kFlipR1[j] : (spar ? kFlipSpcOdd[j] : kFlipSpcEven[j]);
+            const uint32_t nd = n >= 4 ? n >> 2 : 1u;
+            uint32_t acc = 0;
+            for (uint32_t c = 0; c < nd; ++c) {
+                uint32_t nib = sign4(w.ld(s, c));
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (((fm >> q) & 1u) && (sI[q] >> 2) == c)
+                        nib ^= 1u << (sI[q] & 3u);
+                acc |= nib << ((4u * c) & 31u);
+                if (n < 32) {
+                    if (c + 1 == nd)
+                        w.put_row(o, n, acc);
+                } else if (((c + 1) & 7u) == 0) {
+                    w.row()[((o + 4u * c) >> 5) << 6] = acc;
+                    acc = 0;
+                }
+            }
+        }
+    }
+    P = np;
+    (void)frame_ok;
+}
+
+template <int LP, bool I8>
+__global__ void __launch_bounds__(64) scl_char_kernel(KernelArgs a, uint32_t Sl)
+{
+    extern __shared__ uint32_t smem_u[];
+    constexpr uint32_t G = 64 / LP;
+    Wave<LP, I8> w;
+    w.lds = smem_u;
+    w.N = a.N;
+    w.top = a.log2N;
+    w.L = a.L;
+    w.ly = make_layout(a.N, Sl);
+    w.gs = reinterpret_cast<uint32_t*>(a.scratch) + (uint64_t)blockIdx.x * w.ly.gdwords;
+    w.lane = threadIdx.x & 63;
+    w.p = w.lane % LP;
+    w.gb = w.lane - w.p;
+    const uint32_t W = a.N >= 32 ? a.N / 32 : 1u;
+    const uint64_t ngroups = (a.F + G - 1) / G;
+    for (uint64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+        const uint64_t frame = grp * G + w.lane / LP;
+        const bool fok = frame < a.F;
+        const uint64_t fr = fok ? frame : a.F - 1;
+        if constexpr (I8)
+            w.chan = a.llr8 + fr * a.N;
+        else
+            w.chan = a.llr + fr * a.N;
+        w.ptr = 0;
+        w.m = 0;
+        w.right = false;
+        uint32_t P = 1;
+        for (uint32_t k = 0; k < a.nops; ++k) {
+            const uint32_t op = ld_const(a.ops, k);
+            const uint32_t code = op_code(op), s = op_stage(op), o = op_off(op);
+            const bool act = w.p < P;
+            switch (code) {
+            case OP_F:
+                op_fg(w, false, s, o, act);
+                break;
+            case OP_G:
+                op_fg(w, true, s, o, act);
+                break;
+            case OP_COMB:
+                op_comb(w, s, o, act);
+                break;
+            case OP_CS_R0: // RateZeroDecoder :387-421: penalty, bits 0, no branching
+                if (act) {
+                    const uint32_t n = 1u << s, nd = n >= 4 ? n >> 2 : 1u;
+                    int pen = 0;
+                    for (uint32_t c = 0; c < nd; ++c) {
+                        const uint32_t d = w.ld(s, c);
+                        for (uint32_t b = 0; b < 4; ++b)
+                            if (4u * c + b < n) {
+                                const int l = sbyte(d, b);
+                                pen += l < 0 ? l : 0;
+                            }
+                    }
+                    w.m += pen;
+                    if (n >= 32)
+                        for (uint32_t q = 0; q < n / 32; ++q)
+                            w.row()[((o >> 5) + q) << 6] = 0u;
+                    else
+                        w.put_row(o, n, 0u);
+                }
+                break;
+            case OP_CS_R1:
+                op_branch(w, LK_R1, s, o, P, fok);
+                break;
+            case OP_CS_REP:
+                op_branch(w, LK_REP, s, o, P, fok);
+                break;
+            case OP_CS_SPC:
+                op_branch(w, LK_SPC, s, o, P, fok);
+                break;
+            default:
+                break;
+            }
+            wsync();
+        }
+        // extractBestPath (scl_fip_char.cpp:816-856): first path in list order whose
+        // information passes the detector, else path 0
+        const bool act = w.p < P;
+        uint32_t* r = w.row();
+        if (!a.systematic && act) { // re-encode x -> u in place (ButterflyFipPacked transform)
+            for (uint32_t q = 0; q < W; ++q)
+                r[q << 6] = transform_word(r[q << 6], a.N);
+            for (uint32_t d = 1; d < W; d <<= 1)
+                for (uint32_t q = 0; q < W; ++q)
+                    if (!(q & d))
+                        r[q << 6] ^= r[(q + d) << 6];
+        }
+        uint32_t syn = a.crc_c0;
+        if (act && a.crc_bits) {
+            for (uint32_t rb = 0; rb < a.crc_bits; ++rb) {
+                uint32_t pc = 0;
+                for (uint32_t q = 0; q < W; ++q)
+                    pc += __builtin_popcount(r[q << 6] & a.crc_rows[rb * W + q]);
+                syn ^= (pc & 1u) << rb;
+            }
+        }
+        const bool pass = act && syn == 0;
+        const uint64_t bal = ballot(pass);
+        const uint32_t gm = (uint32_t)((bal >> w.gb) & ((LP == 64 ? ~0ull : ((1ull << LP) - 1ull))));
+        const uint32_t win = gm ? (uint32_t)__builtin_ctz(gm) : 0u;
+        wsync();
+        if (fok) {
+            const uint32_t* wr = w.lds + w.ly.bits + (w.gb | win);
+            for (uint32_t b = w.p; b < a.kb; b += LP) {
+                uint32_t byte = 0;
+                for (uint32_t q = 0; q < 8; ++q) {
+                    const uint32_t idx = 8 * b + q;
+                    if (idx < a.K) {
+                        const uint32_t pos = a.info_pos[idx];
+                        byte |= ((wr[(pos >> 5) << 6] >> (pos & 31u)) & 1u) << (7 - q);
+                    }
+                }
+                a.info[frame * a.kb + b] = (uint8_t)byte;
+            }
+            if (w.p == 0 && a.ok)
+                a.ok[frame] = gm ? 1 : 0;
+            if (a.metrics && w.p < a.L)
+                a.metrics[frame * a.L + w.p] = act ? (float)w.m : 0.0f;
+        }
+        wsync();
+    }
+}
+
+template <int LP, bool I8>
+int resident(uint32_t lds_bytes)
+{
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, scl_char_kernel<LP, I8>, 64, lds_bytes) != hipSuccess)
+        n = 0;
+    return n;
+}
+
+uint32_t lp_of(uint32_t L)
+{
+    uint32_t lp = 2;
+    while (lp < L)
+        lp <<= 1;
+    return lp;
+}
+
+} // namespace
+
+// LDS / scratch layout: stages < Sl in LDS, chosen so a wave's LDS stays near
+// PCG_SCLC_LDS_KB (default 24 KB) -- 6 waves per CU.
+int sclc_layout(uint32_t N, uint32_t L, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratch_dwords)
+{
+    if (L < 2 || L > 32 || N < 8)
+        return -4;
+    uint32_t budget = 24u * 1024u;
+    if (const char* e = getenv("PCG_SCLC_LDS_KB"))
+        budget = (uint32_t)atoi(e) * 1024u;
+    const uint32_t top = (uint32_t)__builtin_ctz(N);
+    uint32_t best = 0;
+    for (uint32_t s = 0; s <= top - 1; ++s)
+        if (make_layout(N, s).lds * 4u <= budget)
+            best = s;
+    if (const char* e = getenv("PCG_SCLC_SL"))
+        best = (uint32_t)atoi(e);
+    const Layout y = make_layout(N, best);
+    if (y.lds * 4u > 160u * 1024u)
+        return -4;
+    *lds_dwords = y.lds;
+    *Sl = y.Sl;
+    *scratch_dwords = y.gdwords;
+    return 0;
+}
+
+uint64_t sclc_units(uint64_t F, uint32_t L, uint32_t lds_dwords, bool i8)
+{
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const uint32_t lds = lds_dwords * 4u;
+    int res = 0;
+    switch (lp_of(L)) {
+    case 2: res = i8 ? resident<2, true>(lds) : resident<2, false>(lds); break;
+    case 4: res = i8 ? resident<4, true>(lds) : resident<4, false>(lds); break;
+    case 8: res = i8 ? resident<8, true>(lds) : resident<8, false>(lds); break;
+    case 16: res = i8 ? resident<16, true>(lds) : resident<16, false>(lds); break;
+    default: res = i8 ? resident<32, true>(lds) : resident<32, false>(lds); break;
+    }
+    uint64_t wpc = res > 0 ? (uint64_t)res : 1;
+    if (wpc > 16)
+        wpc = 16;
+    if (const char* e = getenv("PCG_SCLC_WPC"))
+        wpc = (uint64_t)atoi(e);
+    if (getenv("PCG_DEBUG_OCC"))
+        fprintf(stderr, "[pcg] sclc: lds %u B, resident %d waves/CU, using %llu\n", lds, res,
+                (unsigned long long)wpc);
+    const uint64_t G = 64 / lp_of(L);
+    const uint64_t need = (F + G - 1) / G;
+    const uint64_t cap = (uint64_t)cus * wpc;
+    return need < cap ? need : cap;
+}
+
+int launch_scl_char(const KernelArgs& a, hipStream_t stream)
+{
+    const bool i8 = a.llr8 != nullptr;
+    const uint64_t grid = sclc_units(a.F, a.L, a.wave_lds_floats, i8);
+    if (grid == 0)
+        return 0;
+    const size_t lds = (size_t)a.wave_lds_floats * 4u;
+    const uint32_t Sl = a.lds_stage_limit;
+#define PCG_SCLC_LAUNCH(LPV)                                                                                   \
+    if (i8)                                                                                                    \
+        hipLaunchKernelGGL((scl_char_kernel<LPV, true>), dim3((uint32_t)grid), dim3(64), lds, stream, a, Sl);  \
+    else                                                                                                       \
+        hipLaunchKernelGGL((scl_char_kernel<LPV, false>), dim3((uint32_t)grid), dim3(64), lds, stream, a, Sl);
+    switch (lp_of(a.L)) {
+    case 2: PCG_SCLC_LAUNCH(2) break;
+    case 4: PCG_SCLC_LAUNCH(4) break;
+    case 8: PCG_SCLC_LAUNCH(8) break;
+    case 16: PCG_SCLC_LAUNCH(16) break;
+    case 32: PCG_SCLC_LAUNCH(32) break;
+    default: return -4;
+    }
+#undef PCG_SCLC_LAUNCH
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+} // namespace pcg

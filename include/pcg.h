@@ -20,6 +20,12 @@
  *   pcg_decode_f32_host <- the same with host buffers (H2D + decode + D2H)
  *   pcg_plan_create_adaptive <- makeDecoder(..., 2) = AdaptiveFloat, decoder.cpp:75,
  *                        adaptive_float.cpp:14-45 (SC first, SCL for the failures)
+ *   pcg_plan_create_char <- Decoding::create(..., "char") / makeDecoder(..., 0): the 8-bit
+ *                        FastSscFipChar (L = 1, fastssc_fip_char.cpp:573-631) and SclFipChar
+ *                        (L >= 2, scl_fip_char.cpp:759-856), decoder.cpp:37-38, 62-80
+ *   pcg_decode_i8     <- Decoder::decode_vector(const char*, void*) decoder.cpp:169-181,
+ *                        batched, device-resident int8 LLRs
+ *   pcg_decode_i8_host <- the same with host buffers
  *   pcg_plan_destroy  <- Decoder::~Decoder decoder.cpp:104-114
  *   pcg_last_error    <- the std::exception text the reference throws
  *   pcg_puncturer_*   <- PolarCode::Puncturer (include/polarcode/puncturer.h:33-99,
@@ -131,6 +137,41 @@ int pcg_decode_f32_host(pcg_plan* plan,
                         uint8_t* info,
                         uint8_t* ok,
                         float* metrics);
+
+/* An 8-bit fixed-point plan: the reference's "char" decoders (FastSscFipChar for L == 1,
+ * SclFipChar for L >= 2; L <= 32), classified and computed exactly as they are
+ * (saturating int8 LLRs, integer path metrics).  Decode int8 frames with pcg_decode_i8, or
+ * float frames with pcg_decode_f32 (quantised in the kernel as CharContainer::insertLlr
+ * does, bitcontainer.cpp:449-516).  `metrics` of such plans are the integer SCL path
+ * metrics as floats (exact).  Non-systematic decoding follows the reference's intent
+ * (re-encode, then extract); for N < 256 the reference's own output is undefined there
+ * (DESIGN.md Q9). */
+int pcg_plan_create_char(pcg_plan** plan,
+                         uint32_t N,
+                         uint32_t L,
+                         const uint32_t* frozen,
+                         uint32_t n_frozen,
+                         int systematic,
+                         int crc_kind,
+                         int device);
+
+/* Decode F frames of int8 LLRs (device pointer, F x N bytes) with an 8-bit plan; outputs
+ * as pcg_decode_f32.  PCG_E_ARG for a float plan.  Asynchronous. */
+int pcg_decode_i8(pcg_plan* plan,
+                  const int8_t* llr,
+                  uint64_t F,
+                  uint8_t* info,
+                  uint8_t* ok,
+                  float* metrics,
+                  void* stream);
+
+/* Same contract with HOST pointers; synchronous. */
+int pcg_decode_i8_host(pcg_plan* plan,
+                       const int8_t* llr,
+                       uint64_t F,
+                       uint8_t* info,
+                       uint8_t* ok,
+                       float* metrics);
 
 int pcg_plan_describe(const pcg_plan* plan, pcg_plan_desc* desc);
 

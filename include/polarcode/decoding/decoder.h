@@ -31,6 +31,8 @@ protected:
     bool mSystematic = true;
     std::vector<unsigned> mFrozenBits;
     std::vector<float> mLlr;                  ///< setSignal() input (one frame)
+    std::vector<int8_t> mLlr8;                ///< setSignal(const char*) input of 8-bit decoders
+    bool mSignalI8 = false;                   ///< the pending frame is mLlr8
     std::vector<unsigned char> mOutputContainer;
     bool mLastOk = false;
 
@@ -42,6 +44,8 @@ public:
     virtual bool decode() = 0;
     /// setSignal + decode + getDecodedInformationBits (decoder.cpp:154-167).
     bool decode_vector(const float* pLlr, void* pData);
+    /// setSignal(const char*) + decode + getDecodedInformationBits (decoder.cpp:169-181).
+    bool decode_vector(const char* pLlr, void* pData);
     size_t duration_ns() { return mDecoderDuration; }
 
     virtual void initialize(size_t blockLength, const std::vector<unsigned>& frozenBits);
@@ -59,6 +63,9 @@ public:
     }
     virtual size_t getListSize() { return 1; }
     virtual void setSignal(const float* pLlr);
+    /// 8-bit LLRs: float decoders convert them (FloatContainer::insertLlr(const char*),
+    /// bitcontainer.cpp:202-207); 8-bit decoders take them as they are.
+    virtual void setSignal(const char* pLlr);
     void getDecodedInformationBits(void* pData);
 
     /// Batched decode of F frames (host memory): llr F x N, info F x ceil(K/8),
@@ -69,6 +76,9 @@ public:
     /// Same with device pointers, asynchronous on `hipStream` (null = default stream).
     virtual void decodeBatchDevice(const float* llr, size_t F, uint8_t* info, uint8_t* ok = nullptr,
                                    float* metrics = nullptr, void* hipStream = nullptr) = 0;
+    /// Batched decode of F frames of int8 LLRs (host memory).
+    virtual bool decodeBatchI8(const int8_t* llr, size_t F, uint8_t* info, uint8_t* ok = nullptr,
+                               float* metrics = nullptr) = 0;
 };
 
 /// Shared GPU plumbing: owns one pcg_plan, rebuilt when code / detector / systematic
@@ -82,6 +92,7 @@ protected:
     int mPlanKind = -2;
     bool mPlanSys = true;
     bool mAdaptive = false; ///< pcg_plan_create_adaptive (Fast-SSC first, SCL for failures)
+    bool mFixed = false;    ///< pcg_plan_create_char (the reference's 8-bit decoders)
     void ensurePlan();
     void releasePlan();
 
@@ -97,6 +108,14 @@ public:
                      float* metrics = nullptr) override;
     void decodeBatchDevice(const float* llr, size_t F, uint8_t* info, uint8_t* ok = nullptr,
                            float* metrics = nullptr, void* hipStream = nullptr) override;
+    bool decodeBatchI8(const int8_t* llr, size_t F, uint8_t* info, uint8_t* ok = nullptr,
+                       float* metrics = nullptr) override;
+    /// int8 frames in device memory (8-bit decoders only), asynchronous on `hipStream`.
+    void decodeBatchDeviceI8(const int8_t* llr, size_t F, uint8_t* info, uint8_t* ok = nullptr,
+                             float* metrics = nullptr, void* hipStream = nullptr);
+    void setSignal(const char* pLlr) override;
+    using Decoder::setSignal;
+    bool isFixedPoint() const { return mFixed; }
     int device() const { return mDevice; }
 };
 
@@ -132,14 +151,28 @@ public:
                      int device = 0);
 };
 
-/// decoder_impl as in decoder.cpp:54-87: 1 = float (Fast-SSC / SCL), 2 = AdaptiveFloat
-/// (list size >= 2); the "char" (0) and SCAN (3) implementations are not part of this build.
+/// FastSscFipChar (fastssc_fip_char.cpp) on the GPU: 8-bit saturating LLRs.
+class GpuFastSscChar : public GpuDecoder
+{
+public:
+    GpuFastSscChar(size_t blockLength, const std::vector<unsigned>& frozenBits, int device = 0);
+};
+
+/// SclFipChar (scl_fip_char.cpp) on the GPU: 8-bit LLRs, integer path metrics; listSize 2..32.
+class GpuSclChar : public GpuDecoder
+{
+public:
+    GpuSclChar(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits, int device = 0);
+};
+
+/// decoder_impl as in decoder.cpp:54-87: 0 = char (FastSscFipChar / SclFipChar), 1 = float
+/// (Fast-SSC / SCL), 2 = AdaptiveFloat (list size >= 2); SCAN (3) is not part of this build.
 Decoder* makeDecoder(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,
                      int decoder_impl = 1);
 
 /// create (decoder.cpp:26-52).  "gpu" and "float" select the MI355X float decoders
-/// (listSize < 2 -> Fast-SSC).  "char", "mixed" and "scan" are reference decoders
-/// outside this build and raise std::logic_error; unknown strings raise
+/// (listSize < 2 -> Fast-SSC), "char" the 8-bit ones, "mixed" AdaptiveFloat; "scan" is a
+/// reference decoder outside this build and raises std::logic_error; unknown strings raise
 /// std::logic_error("Unknown PolarDecoder type!") exactly as the reference.
 Decoder* create(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,
                 std::string decoderType);
