@@ -8,7 +8,8 @@ and checked by the decoder) through the C ABI (pcg_decode_f32) on the GPU.  Ever
 rank decodes its own batch (independent frames shard with no collective:
 weak scaling); the barrier/max-reduction uses gloo on the host.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--mode scl8|sc|scl32|nr5g|adaptive8]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+                       [--mode scl8|sc|scl32|nr5g|adaptive8|sc_char|scl8_char]
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -29,7 +30,12 @@ MODES = {
                                      "punctured to E=896, device depuncture + SCL L=8, 2^16 frames"),
     "adaptive8": (1024, 512, 8, 1 << 16, "config 3 with the adaptive decoder (AdaptiveFloat): Fast-SSC, "
                                          "then SCL L=8 for CRC-8 failures, N=1024 K=512, 2^16 frames"),
+    "sc_char": (1024, 512, 1, 1 << 16, "config 2 through the 8-bit decoder (FastSscFipChar): int8 LLRs "
+                                       "(amplification 10, pcsim's amp-fixed), N=1024 K=512, 2^16 frames"),
+    "scl8_char": (1024, 512, 8, 1 << 16, "config 3 through the 8-bit decoder (SclFipChar): int8 LLRs "
+                                         "(amplification 10, pcsim's amp-fixed), N=1024 K=512, 2^16 frames"),
 }
+CHAR_AMP = 10.0  # src/simulation/setup.cpp:58 "amp-fixed" (8-bit pre-quantisation scaling)
 NR_E = 896
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec (6.29 TB/s measured float4 copy)
 
@@ -52,13 +58,17 @@ def cpu_baseline(mode, N, L, frozen, llr, threads):
     nr5g the LLRs are the depunctured frames and the reference keeps the CRC-8 its
     makeDecoder installs (it has no CRC-11)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    fixed = mode.endswith("_char")
     try:
         from pyoracle import Reference
         ref = Reference()
         F = llr.shape[0]
         threads = max(1, min(threads, os.cpu_count() or 1))
         t0 = time.time()
-        cw = ref.bench(N, L, frozen, llr, threads=threads, reps=1, crc=8)
+        if fixed:
+            cw = ref.bench_char(N, L, frozen, llr, threads=threads, reps=1, crc=8)
+        else:
+            cw = ref.bench(N, L, frozen, llr, threads=threads, reps=1, crc=8)
         wall = time.time() - t0
         return {"value": cw, "unit": "codewords/s", "cores": threads, "kind": "reference",
                 "sample": f"{F} frames of the same workload, {threads} threads x 1 pass, "
@@ -67,7 +77,15 @@ def cpu_baseline(mode, N, L, frozen, llr, threads):
         from pyoracle import Oracle
         orc = Oracle()
         F = min(llr.shape[0], 4096 if L > 1 else 65536)
-        cw = orc.bench(N, L, frozen, llr[:F], reps=1)
+        if fixed:  # the int8 restatement, timed directly
+            t0 = time.time()
+            if L > 1:
+                orc.sclc_decode(N, L, frozen, llr[:F], crc=8)
+            else:
+                orc.scc_decode(N, frozen, llr[:F], crc=8)
+            cw = F / (time.time() - t0)
+        else:
+            cw = orc.bench(N, L, frozen, llr[:F], reps=1)
         return {"value": cw, "unit": "codewords/s", "cores": 1, "kind": "port",
                 "sample": f"{F} frames of the same workload, 1 thread (oracle restatement)"}
 
@@ -103,7 +121,11 @@ def main():
     else:
         frozen = frozen_bits(N, K, 0.0, "BB")
         llr, info, _ = frames.awgn_frames(N, frozen, F, args.ebn0, seed=1000 + rank, crc=crc)
-    plan = Plan(N, L, frozen, systematic=True, crc=crc, device=local, adaptive=args.mode == "adaptive8")
+    fixed = args.mode.endswith("_char")
+    if fixed:  # pcsim's Scale(amplification) then CharContainer::insertLlr (host side, once)
+        llr = np.clip(np.rint(llr * CHAR_AMP), -128, 127).astype(np.int8)
+    plan = Plan(N, L, frozen, systematic=True, crc=crc, device=local, adaptive=args.mode == "adaptive8",
+                fixed=fixed)
     kb = plan.kb
     d_llr = torch.from_numpy(llr).to(f"cuda:{local}")
     d_info = torch.empty((F, kb), dtype=torch.uint8, device=f"cuda:{local}")
@@ -114,6 +136,8 @@ def main():
     def step():
         if punc is not None:
             plan.decode_punctured_device(punc, d_llr, d_info, d_ok, d_met, stream=stream.cuda_stream)
+        elif fixed:
+            plan.decode_device_i8(d_llr, d_info, d_ok, d_met, stream=stream.cuda_stream)
         else:
             plan.decode_device(d_llr, d_info, d_ok, d_met, stream=stream.cuda_stream)
 
@@ -152,7 +176,7 @@ def main():
 
     if rank == 0:
         # LLRs in (E per frame for nr5g), info bytes + ok flag out (+ metrics below)
-        bytes_per_cw = 4 * (NR_E if punc is not None else N) + kb + 1
+        bytes_per_cw = (1 if fixed else 4) * (NR_E if punc is not None else N) + kb + 1
         if L > 1:
             bytes_per_cw += 4 * L
         achieved = F * bytes_per_cw / (kern_ms * 1e-3) / 1e9
@@ -177,10 +201,11 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": "i8" if fixed else "f32",
             "data": ("synthetic BPSK-AWGN frames (Eb/N0 %.1f dB), " % args.ebn0)
             + ("5G reliability-list frozen set, CRC-11, punctured to E=%d" % NR_E if punc is not None
-               else "BB(0 dB) frozen set, CRC-8"),
+               else "BB(0 dB) frozen set, CRC-8")
+            + (", LLRs x%g quantised to int8" % CHAR_AMP if fixed else ""),
             "config": {"workload": workload, "N": N, "K": K, "L": L, "frames_per_step_per_gpu": F,
                        "crc": "CRC-11" if crc == 11 else "CRC-8", "systematic": True,
                        "parallelism": f"{world} independent shards"},
