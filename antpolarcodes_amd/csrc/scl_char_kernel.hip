@@ -10,9 +10,9 @@
 // Path state of lane l = g*LP + p:
 //   * metric (int32; the reference's `long` metrics are exact integers bounded by
 //     128 N per frame, and every frame starts from 0 -- see DESIGN.md Q8);
-//   * LLR bytes of stages s < top-1, packed 4 per dword, dword c of lane l's column at
+//   * LLR bytes of stages s < top-1 in 16-byte units, unit c of lane l's column at
 //     [(c * 64) + l] of the stage region (LDS for s < Sl, a per-wave global slab for
-//     Sl <= s < top-1), addressed through a 5-bit-per-stage slot table (the lane that
+//     Sl <= s < top-1), so a wave-wide unit access is one contiguous 1 KiB, addressed through a 5-bit-per-stage slot table (the lane that
 //     holds this path's stage s): an F/G rewrites every path's stage s-1 in its own
 //     lane, a branching leaf copies the table of the path a survivor descends from --
 //     the reference's lazy DataPool copy (scl_fip_char.cpp:21-171) without moving LLRs;
@@ -79,14 +79,35 @@ PCG_DEV uint32_t sign4(uint32_t d)
     return ((d >> 7) & 1u) | ((d >> 14) & 2u) | ((d >> 21) & 4u) | ((d >> 28) & 8u);
 }
 
-// stage regions in dwords per lane: stage t has max(1, 2^t / 4) dwords
-__host__ __device__ inline uint32_t st_units(uint32_t s) { return s <= 2 ? s : (1u << (s - 2)) + 1u; }
+// 16 x int8 per lane and unit
+PCG_DEV uint4 f16(const uint4& a, const uint4& b)
+{
+    return make_uint4(f4(a.x, b.x), f4(a.y, b.y), f4(a.z, b.z), f4(a.w, b.w));
+}
+PCG_DEV uint4 g16(const uint4& a, const uint4& b, uint32_t bits16)
+{
+    return make_uint4(g4(a.x, b.x, bits16 & 0xfu), g4(a.y, b.y, (bits16 >> 4) & 0xfu),
+                      g4(a.z, b.z, (bits16 >> 8) & 0xfu), g4(a.w, b.w, (bits16 >> 12) & 0xfu));
+}
+PCG_DEV uint32_t dw_of(const uint4& v, uint32_t k) { return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w)); }
+PCG_DEV int byte_of(const uint4& v, uint32_t i) { return sbyte(dw_of(v, i >> 2), i & 3u); }
+// sign bits of 16 bytes
+PCG_DEV uint32_t sign16(const uint4& v)
+{
+    return sign4(v.x) | (sign4(v.y) << 4) | (sign4(v.z) << 8) | (sign4(v.w) << 12);
+}
+
+// Stage s >= 4 occupies 2^s / 16 units of 16 bytes per lane, unit c of lane l at
+// [(base(s) + c) * 64 + l] (uint4), so a wave-wide unit access is one contiguous 1 KiB;
+// stages 0..3 share unit 0 (stage t at bytes [2^t, 2^(t+1))) and always live in LDS.
+__host__ __device__ inline uint32_t st_units(uint32_t s) { return s <= 3 ? (s ? 1u : 0u) : (1u << (s - 4)); }
+__host__ __device__ inline uint32_t st_base(uint32_t s) { return s <= 3 ? 0u : (1u << (s - 4)); }
 
 struct Layout {
     uint32_t Sl;       // stages < Sl in LDS
-    uint32_t mt;       // first recomputed stage (top-1), stages [Sl, mt) in global scratch
-    uint32_t bits;     // LDS dword offset of the bit rows (64 x W)
-    uint32_t cand;     // LDS dword offset of the candidate lists (2 x 512)
+    uint32_t mt;       // first recomputed stage (top-1); stages [Sl, mt) in global scratch
+    uint32_t bits;     // LDS dword offset of the bit rows (64 x W words)
+    uint32_t cand;     // LDS dword offset of the candidate keys (512 x (metric << 8 | index))
     uint32_t lds;      // LDS dwords per wave
     uint64_t gdwords;  // global scratch dwords per wave
 };
@@ -97,13 +118,149 @@ __host__ __device__ inline Layout make_layout(uint32_t N, uint32_t Sl)
     const uint32_t top = (uint32_t)__builtin_ctz(N);
     y.mt = top - 1;
     y.Sl = Sl < y.mt ? Sl : y.mt;
-    y.bits = 64u * st_units(y.Sl);
+    if (y.Sl < 4)
+        y.Sl = y.mt < 4 ? y.mt : 4; // the shared small-stage unit stays in LDS
+    y.bits = 256u * st_units(y.Sl);
     const uint32_t W = N >= 32 ? N / 32 : 1u;
     y.cand = y.bits + 64u * W;
-    y.lds = y.cand + 1024u;
-    y.gdwords = 64ull * (st_units(y.mt) - st_units(y.Sl));
+    y.lds = y.cand + 512u;
+    y.gdwords = 256ull * (st_units(y.mt) - st_units(y.Sl));
     return y;
 }
+
+// quantise 4 floats as CharContainer::insertLlr does (bitcontainer.cpp:449-516)
+PCG_DEV uint32_t quant4(const float4& v, bool large)
+{
+    const float x[4] = { v.x, v.y, v.z, v.w };
+    uint32_t o = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        int q;
+        if (large) { // convert_f32_to_int8_large: cvtps_epi32 (NaN, |x| >= 2^31 -> INT_MIN) + packs
+            if (!(x[k] < 2147483648.0f) || x[k] < -2147483648.0f) {
+                q = -128;
+            } else {
+                const float r = __builtin_rintf(x[k]);
+                q = r <= -128.0f ? -128 : (r >= 127.0f ? 127 : (int)r);
+            }
+        } else { // vectorizedFtoC (8 <= N < 32)
+            float t = x[k] > -128.0f ? x[k] : -128.0f;
+            t = t < 127.0f ? t : 127.0f;
+            q = (int)__builtin_rintf(t);
+        }
+        o |= ubyte(q, k);
+    }
+    return o;
+}
+
+// ---- stage sources: ld(c) = unit c (16 bytes) of the stage --------------------------
+template <bool I8>
+struct ChanSrc { // the channel frame (stage top)
+    const void* y;
+    uint32_t N;
+    PCG_DEV uint4 ld(uint32_t c) const
+    {
+        if constexpr (I8) {
+            if (N >= 16)
+                return reinterpret_cast<const uint4*>(y)[c];
+            const uint2 v = reinterpret_cast<const uint2*>(y)[0]; // N = 8
+            return make_uint4(v.x, v.y, 0u, 0u);
+        } else {
+            const float4* f = reinterpret_cast<const float4*>(y) + 4u * c;
+            const bool large = N >= 32;
+            if (N >= 16)
+                return make_uint4(quant4(f[0], large), quant4(f[1], large), quant4(f[2], large),
+                                  quant4(f[3], large));
+            return make_uint4(quant4(f[0], large), quant4(f[1], large), 0u, 0u);
+        }
+    }
+};
+// bytes [k, k+16) of a 32-byte window (lo, hi), k a multiple of 4 (N = 16 root split)
+PCG_DEV uint4 shift_units(const uint4& lo, uint32_t k)
+{
+    const uint32_t d[4] = { lo.x, lo.y, lo.z, lo.w };
+    const uint32_t q = k >> 2;
+    return make_uint4(q + 0 < 4 ? d[(q + 0) & 3] : 0u, q + 1 < 4 ? d[(q + 1) & 3] : 0u,
+                      q + 2 < 4 ? d[(q + 2) & 3] : 0u, q + 3 < 4 ? d[(q + 3) & 3] : 0u);
+}
+template <bool I8>
+struct RootSrc { // stage top-1, recomputed: F (left child) or G with the own left-half bits
+    ChanSrc<I8> ch;
+    const uint32_t* row; // own bit row, word w at [w * 64]
+    bool right;
+    PCG_DEV uint4 ld(uint32_t c) const
+    {
+        const uint32_t N = ch.N;
+        uint4 a, b;
+        if (N >= 32) {
+            a = ch.ld(c);
+            b = ch.ld(c + (N >> 5));
+        } else { // N = 8 / 16: the whole frame is in unit 0
+            a = ch.ld(0);
+            b = shift_units(a, N >> 1);
+        }
+        if (!right)
+            return f16(a, b);
+        const uint32_t p0 = 16u * c;
+        const uint32_t w = row[(p0 >> 5) << 6];
+        return g16(a, b, (w >> (p0 & 31u)) & 0xffffu);
+    }
+};
+// 128-bit byte shifts (k = 1, 2, 4, 8)
+PCG_DEV uint4 shr_bytes(const uint4& v, uint32_t k)
+{
+    const uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
+    const uint32_t b = 8u * k;
+    const uint64_t rl = k >= 8 ? hi : ((lo >> b) | (hi << (64u - b))), rh = k >= 8 ? 0ull : (hi >> b);
+    return make_uint4((uint32_t)rl, (uint32_t)(rl >> 32), (uint32_t)rh, (uint32_t)(rh >> 32));
+}
+PCG_DEV uint4 shl_bytes(const uint4& v, uint32_t k)
+{
+    const uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
+    const uint32_t b = 8u * k;
+    const uint64_t rh = k >= 8 ? lo : ((hi << b) | (lo >> (64u - b))), rl = k >= 8 ? 0ull : (lo << b);
+    return make_uint4((uint32_t)rl, (uint32_t)(rl >> 32), (uint32_t)rh, (uint32_t)(rh >> 32));
+}
+struct SmallSrc { // stages 0..3: bytes [2^s, 2^(s+1)) of the shared unit
+    const uint4* b;
+    uint32_t l, k; // k = 2^s
+    PCG_DEV uint4 ld(uint32_t) const { return shr_bytes(b[l], k); }
+};
+struct SmallDst {
+    uint4* b;
+    uint32_t l, k;
+    PCG_DEV void st(uint32_t, const uint4& v) const
+    {
+        const uint4 u = b[l], x = shl_bytes(v, k);
+        // byte mask of [k, 2k)
+        const uint64_t ml = k >= 8 ? 0ull : (((k >= 4 ? 0xffffffffull : ((1ull << (8u * k)) - 1ull))) << (8u * k));
+        const uint64_t mh = k >= 8 ? ~0ull : 0ull;
+        const uint64_t ul = ((uint64_t)u.y << 32) | u.x, uh = ((uint64_t)u.w << 32) | u.z;
+        const uint64_t xl = ((uint64_t)x.y << 32) | x.x, xh = ((uint64_t)x.w << 32) | x.z;
+        const uint64_t rl = (ul & ~ml) | (xl & ml), rh = (uh & ~mh) | (xh & mh);
+        b[l] = make_uint4((uint32_t)rl, (uint32_t)(rl >> 32), (uint32_t)rh, (uint32_t)(rh >> 32));
+    }
+};
+struct LdsSrc {
+    const uint4* b; // stage base
+    uint32_t l;     // lane column
+    PCG_DEV uint4 ld(uint32_t c) const { return b[(c << 6) + l]; }
+};
+struct GlbSrc {
+    const uint4* b;
+    uint32_t l;
+    PCG_DEV uint4 ld(uint32_t c) const { return b[((uint64_t)c << 6) + l]; }
+};
+struct LdsDst {
+    uint4* b;
+    uint32_t l;
+    PCG_DEV void st(uint32_t c, const uint4& v) const { b[(c << 6) + l] = v; }
+};
+struct GlbDst {
+    uint4* b;
+    uint32_t l;
+    PCG_DEV void st(uint32_t c, const uint4& v) const { b[((uint64_t)c << 6) + l] = v; }
+};
 
 template <int LP, bool I8>
 struct Wave {
@@ -124,60 +281,35 @@ struct Wave {
         const uint32_t sh = 5u * s;
         ptr = (ptr & ~(31ull << sh)) | ((uint64_t)p << sh);
     }
-
-    // dword c of the channel frame, quantised (CharContainer::insertLlr) for float input
-    PCG_DEV uint32_t chan_dw(uint32_t c) const
+    PCG_DEV uint4* lds_stage(uint32_t s) const { return reinterpret_cast<uint4*>(lds) + 64u * st_base(s); }
+    PCG_DEV uint4* glb_stage(uint32_t s) const
     {
-        if constexpr (I8) {
-            return reinterpret_cast<const uint32_t*>(chan)[c];
-        } else {
-            const float4 v = reinterpret_cast<const float4*>(chan)[c];
-            const float x[4] = { v.x, v.y, v.z, v.w };
-            uint32_t o = 0;
-#pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) {
-                int q;
-                if (N >= 32) { // convert_f32_to_int8_large: cvtps_epi32 + saturating packs
-                    if (!(x[k] < 2147483648.0f) || x[k] < -2147483648.0f) {
-                        q = -128;
-                    } else {
-                        const float r = __builtin_rintf(x[k]);
-                        q = r <= -128.0f ? -128 : (r >= 127.0f ? 127 : (int)r);
-                    }
-                } else { // vectorizedFtoC
-                    float t = x[k] > -128.0f ? x[k] : -128.0f;
-                    t = t < 127.0f ? t : 127.0f;
-                    q = (int)__builtin_rintf(t);
-                }
-                o |= ubyte(q, k);
-            }
-            return o;
-        }
+        return reinterpret_cast<uint4*>(gs) + 64ull * (st_base(s) - st_units(ly.Sl));
     }
-    // dword c of stage s of this path (any stage <= top)
-    PCG_DEV uint32_t ld(uint32_t s, uint32_t c) const
+    // call f(src) with the source of stage s of this path (uniform branch on s)
+    template <typename Fn>
+    PCG_DEV void with_src(uint32_t s, Fn&& f) const
     {
         if (s == top)
-            return chan_dw(c);
-        if (s == ly.mt) { // recomputed root child
-            const uint32_t a = chan_dw(c), b = chan_dw(c + (N >> 3));
-            if (!right)
-                return f4(a, b);
-            const uint32_t w = row()[((4u * c) >> 5) << 6];
-            return g4(a, b, (w >> ((4u * c) & 31u)) & 0xfu);
-        }
-        const uint32_t l = slot(s);
-        if (s < ly.Sl)
-            return lds[64u * st_units(s) + (c << 6) + l];
-        return gs[64ull * (st_units(s) - st_units(ly.Sl)) + ((uint64_t)c << 6) + l];
-    }
-    // small stages: the whole stage in one dword
-    PCG_DEV void st(uint32_t s, uint32_t c, uint32_t v)
-    {
-        if (s < ly.Sl)
-            lds[64u * st_units(s) + (c << 6) + lane] = v;
+            f(ChanSrc<I8>{ chan, N });
+        else if (s == ly.mt)
+            f(RootSrc<I8>{ ChanSrc<I8>{ chan, N }, row(), right });
+        else if (s <= 3)
+            f(SmallSrc{ lds_stage(0), slot(s), 1u << s });
+        else if (s < ly.Sl)
+            f(LdsSrc{ lds_stage(s), slot(s) });
         else
-            gs[64ull * (st_units(s) - st_units(ly.Sl)) + ((uint64_t)c << 6) + lane] = v;
+            f(GlbSrc{ glb_stage(s), slot(s) });
+    }
+    template <typename Fn>
+    PCG_DEV void with_dst(uint32_t s, Fn&& f) const
+    {
+        if (s <= 3)
+            f(SmallDst{ lds_stage(0), lane, 1u << s });
+        else if (s < ly.Sl)
+            f(LdsDst{ lds_stage(s), lane });
+        else
+            f(GlbDst{ glb_stage(s), lane });
     }
     // packed bits [o, o+c) of the own row, c <= 32 and inside one word
     PCG_DEV uint32_t bits_at(uint32_t o, uint32_t c) const
@@ -207,23 +339,42 @@ PCG_DEV void op_fg(Wave<LP, I8>& w, bool g, uint32_t s, uint32_t o, bool act)
         return;
     }
     if (act) {
-        if (h >= 4) {
-            const uint32_t hq = h >> 2;
-            for (uint32_t c = 0; c < hq; ++c) {
-                const uint32_t a = w.ld(s, c), b = w.ld(s, c + hq);
-                const uint32_t v = g ? g4(a, b, w.bits_at(o + 4u * c, 4)) : f4(a, b);
-                w.st(cs, c, v);
-            }
-        } else { // h = 1, 2: stage s is 2h bytes of one dword
-            const uint32_t d = w.ld(s, 0);
-            const uint32_t nib = g ? w.bits_at(o, h) : 0u;
-            uint32_t v = 0;
-            for (uint32_t k = 0; k < h; ++k) {
-                const int l = sbyte(d, k), r = sbyte(d, k + h);
-                v |= ubyte(g ? fip_g(l, r, (nib >> k) & 1u) : fip_f(l, r), k);
-            }
-            w.st(cs, 0, v);
-        }
+        w.with_src(s, [&](const auto& src) {
+            w.with_dst(cs, [&](const auto& dst) {
+                if (h >= 16) {
+                    const uint32_t hq = h >> 4;
+                    uint32_t c = 0;
+                    for (; c + 2 <= hq; c += 2) { // two units in flight
+                        const uint4 a0 = src.ld(c), b0 = src.ld(c + hq), a1 = src.ld(c + 1), b1 = src.ld(c + 1 + hq);
+                        if (g) {
+                            const uint32_t bb = w.bits_at(o + 16u * c, 32);
+                            dst.st(c, g16(a0, b0, bb & 0xffffu));
+                            dst.st(c + 1, g16(a1, b1, bb >> 16));
+                        } else {
+                            dst.st(c, f16(a0, b0));
+                            dst.st(c + 1, f16(a1, b1));
+                        }
+                    }
+                    if (c < hq) { // hq == 1
+                        const uint4 a = src.ld(c), b = src.ld(c + hq);
+                        dst.st(c, g ? g16(a, b, w.bits_at(o + 16u * c, 16)) : f16(a, b));
+                    }
+                } else { // h = 1..8: stage s is 2h bytes of one unit
+                    const uint4 d = src.ld(0);
+                    const uint32_t nib = g ? w.bits_at(o, h) : 0u;
+                    uint32_t v[2] = { 0u, 0u };
+                    for (uint32_t k = 0; k < h; ++k) {
+                        const int l = byte_of(d, k), r = byte_of(d, k + h);
+                        const uint32_t q = ubyte(g ? fip_g(l, r, (nib >> k) & 1u) : fip_f(l, r), k & 3u);
+                        if (k < 4)
+                            v[0] |= q;
+                        else
+                            v[1] |= q;
+                    }
+                    dst.st(0, make_uint4(v[0], v[1], 0u, 0u));
+                }
+            });
+        });
     }
     w.own(cs);
 }
@@ -265,40 +416,42 @@ PCG_DEV void weak_llrs(const Wave<LP, I8>& w, uint32_t s, uint32_t n, int (&T)[K
         si[k] = 0xffffffffu;
     }
     par = 0;
-    const uint32_t nd = n >= 4 ? n >> 2 : 1u;
-    for (uint32_t c = 0; c < nd; ++c) {
-        const uint32_t d = w.ld(s, c);
+    w.with_src(s, [&](const auto& src) {
+        const uint32_t nu = n >= 16 ? n >> 4 : 1u;
+        for (uint32_t c = 0; c < nu; ++c) {
+            const uint4 d = src.ld(c);
 #pragma unroll
-        for (uint32_t b = 0; b < 4; ++b) {
-            const uint32_t i = 4u * c + b;
-            if (i < n) {
-                const int l = sbyte(d, b);
-                par ^= l < 0 ? 1u : 0u;
-                int t = l > -127 ? l : -127;
-                t = t < 0 ? -t : t;
-                if (i < lim) {
+            for (uint32_t b = 0; b < 16; ++b) {
+                const uint32_t i = 16u * c + b;
+                if (i < n) {
+                    const int l = byte_of(d, b);
+                    par ^= l < 0 ? 1u : 0u;
+                    int t = l > -127 ? l : -127;
+                    t = t < 0 ? -t : t;
+                    if (i < lim) {
 #pragma unroll
-                    for (int k = 0; k < KW; ++k)
-                        if ((uint32_t)k == i)
-                            v0[k] = t;
-                } else if (t < sv[KW - 1]) { // stable insertion into the sorted set
+                        for (int k = 0; k < KW; ++k)
+                            if ((uint32_t)k == i)
+                                v0[k] = t;
+                    } else if (t < sv[KW - 1]) { // stable insertion into the sorted set
 #pragma unroll
-                    for (int k = KW - 1; k >= 0; --k) {
-                        const bool shift = k > 0 && t < sv[k > 0 ? k - 1 : 0];
-                        if (t < sv[k]) {
-                            if (shift) {
-                                sv[k] = sv[k - 1];
-                                si[k] = si[k - 1];
-                            } else {
-                                sv[k] = t;
-                                si[k] = i;
+                        for (int k = KW - 1; k >= 0; --k) {
+                            const bool shift = k > 0 && t < sv[k > 0 ? k - 1 : 0];
+                            if (t < sv[k]) {
+                                if (shift) {
+                                    sv[k] = sv[k - 1];
+                                    si[k] = si[k - 1];
+                                } else {
+                                    sv[k] = t;
+                                    si[k] = i;
+                                }
                             }
                         }
                     }
                 }
             }
         }
-    }
+    });
     // literal swap-selection on the candidate elements: e < KW: position e (value v0),
     // e >= KW: the sorted set (position = index si)
     int ev[2 * KW];
@@ -377,8 +530,8 @@ PCG_DEV void op_branch(Wave<LP, I8>& w, uint32_t kind, uint32_t s, uint32_t o, u
     const uint32_t k = kind == LK_R1 ? 4u : (kind == LK_REP ? 2u : 8u);
     const uint32_t lk = kind == LK_R1 ? 2u : (kind == LK_REP ? 1u : 3u);
     const bool act = w.p < P;
-    int* V = reinterpret_cast<int*>(w.lds + w.ly.cand) + (w.gb / LP) * (8 * LP);
-    uint32_t* ID = w.lds + w.ly.cand + 512u + (w.gb / LP) * (8 * LP);
+    // candidate keys metric << 8 | index (|metric| < 2^23 for N <= 32768, index < 256)
+    int* KV = reinterpret_cast<int*>(w.lds + w.ly.cand) + (w.gb / LP) * (8 * LP);
     int T[4] = { 0, 0, 0, 0 };
     uint32_t I[4] = { 0, 0, 0, 0 }, par = 0;
     if (act) {
@@ -386,16 +539,19 @@ PCG_DEV void op_branch(Wave<LP, I8>& w, uint32_t kind, uint32_t s, uint32_t o, u
         const int m = w.m;
         if (kind == LK_REP) {
             int z = 0, on = 0;
-            const uint32_t nd = n >= 4 ? n >> 2 : 1u;
-            for (uint32_t cc = 0; cc < nd; ++cc) {
-                const uint32_t d = w.ld(s, cc);
-                for (uint32_t b = 0; b < 4; ++b)
-                    if (4u * cc + b < n) {
-                        const int l = sbyte(d, b);
-                        z += l < 0 ? l : 0;
-                        on += l > 0 ? l : 0;
-                    }
-            }
+            w.with_src(s, [&](const auto& src) {
+                const uint32_t nu = n >= 16 ? n >> 4 : 1u;
+                for (uint32_t cc = 0; cc < nu; ++cc) {
+                    const uint4 d = src.ld(cc);
+#pragma unroll
+                    for (uint32_t b = 0; b < 16; ++b)
+                        if (16u * cc + b < n) {
+                            const int l = byte_of(d, b);
+                            z += l < 0 ? l : 0;
+                            on += l > 0 ? l : 0;
+                        }
+                }
+            });
             c[0] = m + z;
             c[1] = m - on;
         } else if (kind == LK_R1) {
@@ -426,10 +582,8 @@ PCG_DEV void op_branch(Wave<LP, I8>& w, uint32_t kind, uint32_t s, uint32_t o, u
             c[6] = mm - T[2] - T[3];
             c[7] = mm - wk - T[1] - T[2] - T[3];
         }
-        for (uint32_t j = 0; j < k; ++j) {
-            V[w.p * k + j] = c[j];
-            ID[w.p * k + j] = w.p * k + j;
-        }
+        for (uint32_t j = 0; j < k; ++j)
+            KV[w.p * k + j] = (int)(((uint32_t)c[j] << 8) | (w.p * k + j));
     }
     wsync();
     // simplePartialSortDescending(idx, metrics, np, size) (arrayfuncs.h:161-183)
@@ -439,7 +593,7 @@ PCG_DEV void op_branch(Wave<LP, I8>& w, uint32_t kind, uint32_t s, uint32_t o, u
         int bv = INT_NEG;
         uint32_t bq = 0xffffffffu;
         for (uint32_t q = i + w.p; q < size; q += LP) {
-            const int v = V[q];
+            const int v = KV[q] >> 8;
             if (bq == 0xffffffffu || v > bv) {
                 bv = v;
                 bq = q;
@@ -447,19 +601,17 @@ PCG_DEV void op_branch(Wave<LP, I8>& w, uint32_t kind, uint32_t s, uint32_t o, u
         }
         grp_argmax_i<LP>(bv, bq);
         if (w.p == 0 && bq != i) {
-            const int tv = V[i];
-            const uint32_t ti = ID[i];
-            V[i] = V[bq];
-            ID[i] = ID[bq];
-            V[bq] = tv;
-            ID[bq] = ti;
+            const int t = KV[i];
+            KV[i] = KV[bq];
+            KV[bq] = t;
         }
         wsync();
     }
     // survivors
     const bool surv = w.p < np;
-    const uint32_t id = surv ? ID[w.p] : 0u;
-    const int nm = surv ? V[w.p] : 0;
+    const int key = surv ? KV[w.p] : 0;
+    const uint32_t id = (uint32_t)key & 0xffu;
+    const int nm = key >> 8;
     wsync();
     const uint32_t src = id >> lk, j = id & (k - 1u);
     const uint32_t sl = w.gb | src;
@@ -500,23 +652,24 @@ PCG_DEV void op_branch(Wave<LP, I8>& w, uint32_t kind, uint32_t s, uint32_t o, u
                 w.put_row(o, n, v);
         } else {
             const uint32_t fm = kind == LK_R1 ? kFlipR1[j] : (spar ? kFlipSpcOdd[j] : kFlipSpcEven[j]);
-            const uint32_t nd = n >= 4 ? n >> 2 : 1u;
-            uint32_t acc = 0;
-            for (uint32_t c = 0; c < nd; ++c) {
-                uint32_t nib = sign4(w.ld(s, c));
+            w.with_src(s, [&](const auto& src) {
+                const uint32_t nu = n >= 16 ? n >> 4 : 1u;
+                uint32_t acc = 0;
+                for (uint32_t c = 0; c < nu; ++c) {
+                    uint32_t sg = sign16(src.ld(c));
 #pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    if (((fm >> q) & 1u) && (sI[q] >> 2) == c)
-                        nib ^= 1u << (sI[q] & 3u);
-                acc |= nib << ((4u * c) & 31u);
-                if (n < 32) {
-                    if (c + 1 == nd)
-                        w.put_row(o, n, acc);
-                } else if (((c + 1) & 7u) == 0) {
-                    w.row()[((o + 4u * c) >> 5) << 6] = acc;
-                    acc = 0;
+                    for (int q = 0; q < 4; ++q)
+                        if (((fm >> q) & 1u) && (sI[q] >> 4) == c)
+                            sg ^= 1u << (sI[q] & 15u);
+                    if (n < 32) {
+                        w.put_row(o, n, sg);
+                    } else if (c & 1u) {
+                        w.row()[((o + 16u * c) >> 5) << 6] = acc | (sg << 16);
+                    } else {
+                        acc = sg;
+                    }
                 }
-            }
+            });
         }
     }
     P = np;
@@ -568,16 +721,20 @@ __global__ void __launch_bounds__(64) scl_char_kernel(KernelArgs a, uint32_t Sl)
                 break;
             case OP_CS_R0: // RateZeroDecoder :387-421: penalty, bits 0, no branching
                 if (act) {
-                    const uint32_t n = 1u << s, nd = n >= 4 ? n >> 2 : 1u;
+                    const uint32_t n = 1u << s;
                     int pen = 0;
-                    for (uint32_t c = 0; c < nd; ++c) {
-                        const uint32_t d = w.ld(s, c);
-                        for (uint32_t b = 0; b < 4; ++b)
-                            if (4u * c + b < n) {
-                                const int l = sbyte(d, b);
-                                pen += l < 0 ? l : 0;
-                            }
-                    }
+                    w.with_src(s, [&](const auto& src) {
+                        const uint32_t nu = n >= 16 ? n >> 4 : 1u;
+                        for (uint32_t c = 0; c < nu; ++c) {
+                            const uint4 d = src.ld(c);
+#pragma unroll
+                            for (uint32_t b = 0; b < 16; ++b)
+                                if (16u * c + b < n) {
+                                    const int l = byte_of(d, b);
+                                    pen += l < 0 ? l : 0;
+                                }
+                        }
+                    });
                     w.m += pen;
                     if (n >= 32)
                         for (uint32_t q = 0; q < n / 32; ++q)
@@ -667,13 +824,13 @@ uint32_t lp_of(uint32_t L)
 
 } // namespace
 
-// LDS / scratch layout: stages < Sl in LDS, chosen so a wave's LDS stays near
-// PCG_SCLC_LDS_KB (default 24 KB) -- 6 waves per CU.
+// LDS / scratch layout: stages < Sl in LDS, chosen so a wave's LDS stays within
+// PCG_SCLC_LDS_KB (default 20 KB: 8 waves per CU, measured best at N = 1024, L = 8).
 int sclc_layout(uint32_t N, uint32_t L, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratch_dwords)
 {
     if (L < 2 || L > 32 || N < 8)
         return -4;
-    uint32_t budget = 24u * 1024u;
+    uint32_t budget = 20u * 1024u;
     if (const char* e = getenv("PCG_SCLC_LDS_KB"))
         budget = (uint32_t)atoi(e) * 1024u;
     const uint32_t top = (uint32_t)__builtin_ctz(N);
