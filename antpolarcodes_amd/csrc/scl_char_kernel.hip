@@ -57,22 +57,56 @@ PCG_DEV int fip_f(int l, int r)
 }
 PCG_DEV int fip_g(int l, int r, uint32_t bit) { return sat8(bit ? r - l : r + l); }
 
+// ---- 4 bytes per dword with packed 16-bit ops ----------------------------------------
+// Each byte is placed in the high byte of a 16-bit lane (low byte 0): even bytes (0, 2)
+// and odd bytes (1, 3) form two v_pk_*_i16 pairs.  In this form int16 saturation is the
+// reference's int8 saturation (_mm256_adds_epi8 / subs_epi8) and the result byte is the
+// high byte of each lane.
+typedef short s2_t __attribute__((ext_vector_type(2)));
+PCG_DEV s2_t as_s2(uint32_t x) { return __builtin_bit_cast(s2_t, x); }
+PCG_DEV uint32_t as_u(s2_t x) { return __builtin_bit_cast(uint32_t, x); }
+PCG_DEV uint32_t hb_even(uint32_t a) { return __builtin_amdgcn_perm(0u, a, 0x020c000cu); }
+PCG_DEV uint32_t hb_odd(uint32_t a) { return a & 0xff00ff00u; }
+PCG_DEV uint32_t hb_pack(uint32_t even, uint32_t odd) { return __builtin_amdgcn_perm(odd, even, 0x07030501u); }
+
+// F_function_calc (fip_char.h:35-56): sign(l)^sign(r) * max(1, min(|max(l,-127)|, |max(r,-127)|))
+PCG_DEV uint32_t f_pair(uint32_t l, uint32_t r)
+{
+    const s2_t a = as_s2(l), b = as_s2(r), z = { 0, 0 };
+    const s2_t aa = __builtin_elementwise_max(a, __builtin_elementwise_sub_sat(z, a));
+    const s2_t ab = __builtin_elementwise_max(b, __builtin_elementwise_sub_sat(z, b));
+    s2_t m = __builtin_elementwise_min(aa, ab);
+    m = __builtin_elementwise_min(m, (s2_t){ 0x7f00, 0x7f00 }); // |max(x, -127)| = min(|x|, 127)
+    m = __builtin_elementwise_max(m, (s2_t){ 0x100, 0x100 });
+    const s2_t sg = as_s2(l ^ r) >> (s2_t){ 15, 15 };
+    return as_u(as_s2(as_u(m) ^ as_u(sg)) - sg);
+}
 PCG_DEV uint32_t f4(uint32_t a, uint32_t b)
 {
-    uint32_t o = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k)
-        o |= ubyte(fip_f(sbyte(a, k), sbyte(b, k)), k);
-    return o;
+    return hb_pack(f_pair(hb_even(a), hb_even(b)), f_pair(hb_odd(a), hb_odd(b)));
 }
-PCG_DEV uint32_t g4(uint32_t a, uint32_t b, uint32_t nib)
+// G_function_calc (fip_char.h:58-64): bit ? sat(r - l) : sat(r + l); `bits` bit k <-> byte k
+PCG_DEV uint32_t g_pair(uint32_t l, uint32_t r, uint32_t msk)
 {
-    uint32_t o = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; ++k)
-        o |= ubyte(fip_g(sbyte(a, k), sbyte(b, k), (nib >> k) & 1u), k);
-    return o;
+    const s2_t a = as_s2(l), b = as_s2(r);
+    const uint32_t sum = as_u(__builtin_elementwise_add_sat(b, a)), dif = as_u(__builtin_elementwise_sub_sat(b, a));
+    return (dif & msk) | (sum & ~msk);
 }
+PCG_DEV uint32_t bitmask2(uint32_t bits, uint32_t k0)
+{ // 16-bit lane masks from bits k0 and k0 + 2
+    const uint32_t m0 = (uint32_t)__builtin_amdgcn_sbfe((int)bits, k0, 1);
+    const uint32_t m1 = (uint32_t)__builtin_amdgcn_sbfe((int)bits, k0 + 2, 1);
+    return (m0 & 0x0000ffffu) | (m1 & 0xffff0000u);
+}
+PCG_DEV uint32_t g4b(uint32_t a, uint32_t b, uint32_t bits, uint32_t k0)
+{
+    return hb_pack(g_pair(hb_even(a), hb_even(b), bitmask2(bits, k0)),
+                   g_pair(hb_odd(a), hb_odd(b), bitmask2(bits, k0 + 1)));
+}
+PCG_DEV uint32_t g4(uint32_t a, uint32_t b, uint32_t nib) { return g4b(a, b, nib, 0); }
+// sums over the 4 signed bytes of a dword: sum of x and sum of |x| (v_dot4 / v_sad_u8)
+PCG_DEV int bsum(uint32_t a) { return __builtin_amdgcn_sdot4((int)a, 0x01010101, 0, false); }
+PCG_DEV int babs(uint32_t a) { return (int)__builtin_amdgcn_sad_u8(a ^ 0x80808080u, 0x80808080u, 0u); }
 // sign bits of 4 bytes as a nibble
 PCG_DEV uint32_t sign4(uint32_t d)
 {
@@ -86,8 +120,8 @@ PCG_DEV uint4 f16(const uint4& a, const uint4& b)
 }
 PCG_DEV uint4 g16(const uint4& a, const uint4& b, uint32_t bits16)
 {
-    return make_uint4(g4(a.x, b.x, bits16 & 0xfu), g4(a.y, b.y, (bits16 >> 4) & 0xfu),
-                      g4(a.z, b.z, (bits16 >> 8) & 0xfu), g4(a.w, b.w, (bits16 >> 12) & 0xfu));
+    return make_uint4(g4b(a.x, b.x, bits16, 0), g4b(a.y, b.y, bits16, 4), g4b(a.z, b.z, bits16, 8),
+                      g4b(a.w, b.w, bits16, 12));
 }
 PCG_DEV uint32_t dw_of(const uint4& v, uint32_t k) { return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w)); }
 PCG_DEV int byte_of(const uint4& v, uint32_t i) { return sbyte(dw_of(v, i >> 2), i & 3u); }
@@ -540,16 +574,22 @@ PCG_DEV void op_branch(Wave<LP, I8>& w, uint32_t kind, uint32_t s, uint32_t o, u
         if (kind == LK_REP) {
             int z = 0, on = 0;
             w.with_src(s, [&](const auto& src) {
-                const uint32_t nu = n >= 16 ? n >> 4 : 1u;
-                for (uint32_t cc = 0; cc < nu; ++cc) {
-                    const uint4 d = src.ld(cc);
-#pragma unroll
-                    for (uint32_t b = 0; b < 16; ++b)
-                        if (16u * cc + b < n) {
-                            const int l = byte_of(d, b);
-                            z += l < 0 ? l : 0;
-                            on += l > 0 ? l : 0;
-                        }
+                if (n >= 16) { // sum min(l,0), sum max(l,0) from sum l and sum |l|
+                    int sl = 0, sa = 0;
+                    for (uint32_t cc = 0; cc < (n >> 4); ++cc) {
+                        const uint4 d = src.ld(cc);
+                        sl += bsum(d.x) + bsum(d.y) + bsum(d.z) + bsum(d.w);
+                        sa += babs(d.x) + babs(d.y) + babs(d.z) + babs(d.w);
+                    }
+                    z = (sl - sa) / 2;
+                    on = (sl + sa) / 2;
+                } else {
+                    const uint4 d = src.ld(0);
+                    for (uint32_t b = 0; b < n; ++b) {
+                        const int l = byte_of(d, b);
+                        z += l < 0 ? l : 0;
+                        on += l > 0 ? l : 0;
+                    }
                 }
             });
             c[0] = m + z;
@@ -724,15 +764,20 @@ __global__ void __launch_bounds__(64) scl_char_kernel(KernelArgs a, uint32_t Sl)
                     const uint32_t n = 1u << s;
                     int pen = 0;
                     w.with_src(s, [&](const auto& src) {
-                        const uint32_t nu = n >= 16 ? n >> 4 : 1u;
-                        for (uint32_t c = 0; c < nu; ++c) {
-                            const uint4 d = src.ld(c);
-#pragma unroll
-                            for (uint32_t b = 0; b < 16; ++b)
-                                if (16u * c + b < n) {
-                                    const int l = byte_of(d, b);
-                                    pen += l < 0 ? l : 0;
-                                }
+                        if (n >= 16) { // sum min(l, 0) = (sum l - sum |l|) / 2
+                            int sl = 0, sa = 0;
+                            for (uint32_t c = 0; c < (n >> 4); ++c) {
+                                const uint4 d = src.ld(c);
+                                sl += bsum(d.x) + bsum(d.y) + bsum(d.z) + bsum(d.w);
+                                sa += babs(d.x) + babs(d.y) + babs(d.z) + babs(d.w);
+                            }
+                            pen = (sl - sa) / 2;
+                        } else {
+                            const uint4 d = src.ld(0);
+                            for (uint32_t b = 0; b < n; ++b) {
+                                const int l = byte_of(d, b);
+                                pen += l < 0 ? l : 0;
+                            }
                         }
                     });
                     w.m += pen;
