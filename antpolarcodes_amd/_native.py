@@ -9,7 +9,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libpcg.so")
+LIB_PATH = os.environ.get("PCG_DEV_LIB") or os.path.join(_HERE, "lib", "libpcg.so")  # PCG_DEV_LIB: dev builds
 
 PCG_OK = 0
 PCG_E_ARG = -1

@@ -39,6 +39,22 @@ namespace {
 
 constexpr int INT_NEG = -2147483647 - 1;
 
+// dev-only per-phase cycle profile (build with -DPCG_SCLC_PROF, run with PCG_OPPROF=1;
+// tools/sclc_prof.py): buckets 1 F, 2 G, 4 COMB, 16 R0, 17 R1, 18 Rep, 19 SPC
+// (candidates), 20 pruning, 21 survivors, 22 final extraction, 61 total, 62 groups
+#ifdef PCG_SCLC_PROF
+#define SC_T0(v) const uint64_t v = __builtin_amdgcn_s_memtime()
+#define SC_ADD(prof, b, t0)                                                                    \
+    do {                                                                                       \
+        const uint64_t _t1 = __builtin_amdgcn_s_memtime();                                     \
+        if ((prof) && (threadIdx.x & 63) == 0)                                                 \
+            atomicAdd(&(prof)[(b)], (unsigned long long)(_t1 - (t0)));                         \
+    } while (0)
+#else
+#define SC_T0(v) (void)0
+#define SC_ADD(prof, b, t0) (void)0
+#endif
+
 PCG_DEV int sat8(int v) { return v < -128 ? -128 : (v > 127 ? 127 : v); }
 PCG_DEV int sbyte(uint32_t d, uint32_t b) { return (int)(int8_t)(uint8_t)(d >> (8 * b)); }
 PCG_DEV uint32_t ubyte(int v, uint32_t b) { return ((uint32_t)v & 0xffu) << (8 * b); }
@@ -140,8 +156,8 @@ __host__ __device__ inline uint32_t st_base(uint32_t s) { return s <= 3 ? 0u : (
 struct Layout {
     uint32_t Sl;       // stages < Sl in LDS
     uint32_t mt;       // first recomputed stage (top-1); stages [Sl, mt) in global scratch
-    uint32_t bits;     // LDS dword offset of the bit rows (64 x W words)
-    uint32_t cand;     // LDS dword offset of the candidate keys (512 x (metric << 8 | index))
+    uint32_t bits;     // LDS dword offset of the bit rows (word w of lane l at [w * 64 + l])
+    uint32_t cand;     // LDS dword offset of the candidate keys (G groups x 9 LP x (metric << 8 | index))
     uint32_t lds;      // LDS dwords per wave
     uint64_t gdwords;  // global scratch dwords per wave
 };
@@ -157,7 +173,7 @@ __host__ __device__ inline Layout make_layout(uint32_t N, uint32_t Sl)
     y.bits = 256u * st_units(y.Sl);
     const uint32_t W = N >= 32 ? N / 32 : 1u;
     y.cand = y.bits + 64u * W;
-    y.lds = y.cand + 512u;
+    y.lds = y.cand + 576u;
     y.gdwords = 256ull * (st_units(y.mt) - st_units(y.Sl));
     return y;
 }
@@ -307,6 +323,7 @@ struct Wave {
     uint64_t ptr = 0;   // slot of stage s at bits 5s
     int m = 0;          // path metric
     bool right = false; // root's right child active (recomputed stage top-1 = G)
+    unsigned long long* prof = nullptr;
 
     PCG_DEV uint32_t* row() const { return lds + ly.bits + lane; } // word w at [w * 64]
     PCG_DEV uint32_t slot(uint32_t s) const { return gb | (uint32_t)((ptr >> (5u * s)) & 31u); }
@@ -539,18 +556,26 @@ __constant__ uint8_t kFlipR1[4] = { 0x0, 0x1, 0x2, 0x3 };
 __constant__ uint8_t kFlipSpcOdd[8] = { 0x1, 0x2, 0x4, 0x8, 0x7, 0xB, 0xD, 0xE };
 __constant__ uint8_t kFlipSpcEven[8] = { 0x0, 0x3, 0x5, 0x9, 0x6, 0xA, 0xC, 0xF };
 
+template <int D>
+PCG_DEV void argmax_i_step(int& v, uint32_t& q)
+{
+    const int ov = (int)bfly<D>((uint32_t)v);
+    const uint32_t oq = bfly<D>(q);
+    if (ov > v || (ov == v && oq < q)) {
+        v = ov;
+        q = oq;
+    }
+}
+// (max, lowest position) over the LP lanes of a group: DPP / permlane butterflies
+// (mirror partners are fine for this idempotent, commutative combine)
 template <int LP>
 PCG_DEV void grp_argmax_i(int& v, uint32_t& q)
 {
-#pragma unroll
-    for (int d = 1; d < LP; d <<= 1) {
-        const int ov = __shfl_xor(v, d, 64);
-        const uint32_t oq = __shfl_xor(q, d, 64);
-        if (ov > v || (ov == v && oq < q)) {
-            v = ov;
-            q = oq;
-        }
-    }
+    if constexpr (LP > 1) argmax_i_step<1>(v, q);
+    if constexpr (LP > 2) argmax_i_step<2>(v, q);
+    if constexpr (LP > 4) argmax_i_step<4>(v, q);
+    if constexpr (LP > 8) argmax_i_step<8>(v, q);
+    if constexpr (LP > 16) argmax_i_step<16>(v, q);
 }
 
 enum { LK_R1 = 0, LK_REP = 1, LK_SPC = 2 };
@@ -564,8 +589,10 @@ PCG_DEV void op_branch(Wave<LP, I8>& w, uint32_t kind, uint32_t s, uint32_t o, u
     const uint32_t k = kind == LK_R1 ? 4u : (kind == LK_REP ? 2u : 8u);
     const uint32_t lk = kind == LK_R1 ? 2u : (kind == LK_REP ? 1u : 3u);
     const bool act = w.p < P;
+    SC_T0(tb0);
     // candidate keys metric << 8 | index (|metric| < 2^23 for N <= 32768, index < 256)
-    int* KV = reinterpret_cast<int*>(w.lds + w.ly.cand) + (w.gb / LP) * (8 * LP);
+    // group stride 9 LP: the 64/LP groups' lanes hit distinct LDS banks in the pruning scans
+    int* KV = reinterpret_cast<int*>(w.lds + w.ly.cand) + (w.gb / LP) * (9 * LP);
     int T[4] = { 0, 0, 0, 0 };
     uint32_t I[4] = { 0, 0, 0, 0 }, par = 0;
     if (act) {
@@ -626,6 +653,8 @@ PCG_DEV void op_branch(Wave<LP, I8>& w, uint32_t kind, uint32_t s, uint32_t o, u
             KV[w.p * k + j] = (int)(((uint32_t)c[j] << 8) | (w.p * k + j));
     }
     wsync();
+    SC_ADD(w.prof, 17 + kind, tb0);
+    SC_T0(tb1);
     // simplePartialSortDescending(idx, metrics, np, size) (arrayfuncs.h:161-183)
     const uint32_t size = k * P, np = size < w.L ? size : w.L;
     const uint32_t lim = size - 1 < np ? size - 1 : np;
@@ -647,6 +676,8 @@ PCG_DEV void op_branch(Wave<LP, I8>& w, uint32_t kind, uint32_t s, uint32_t o, u
         }
         wsync();
     }
+    SC_ADD(w.prof, 20, tb1);
+    SC_T0(tb2);
     // survivors
     const bool surv = w.p < np;
     const int key = surv ? KV[w.p] : 0;
@@ -661,19 +692,19 @@ PCG_DEV void op_branch(Wave<LP, I8>& w, uint32_t kind, uint32_t s, uint32_t o, u
 #pragma unroll
     for (int q = 0; q < 4; ++q)
         sI[q] = __shfl(I[q], (int)sl, 64);
-    // codeword prefix [0, o) from the source path (read all, then write)
+    // codeword prefix [0, o) from the source path (read a batch, then write it)
     const uint32_t W = w.N >= 32 ? w.N / 32 : 1u;
     const uint32_t pw = (o + 31u) >> 5;
     uint32_t* rowb = w.lds + w.ly.bits;
-    for (uint32_t b0 = 0; b0 < pw; b0 += 8) {
-        uint32_t t[8];
+    for (uint32_t b0 = 0; b0 < pw; b0 += 16) {
+        uint32_t t[16];
 #pragma unroll
-        for (uint32_t q = 0; q < 8; ++q)
+        for (uint32_t q = 0; q < 16; ++q)
             t[q] = (b0 + q < pw && b0 + q < W) ? rowb[((b0 + q) << 6) + sl] : 0u;
         wsync();
         if (surv && src != w.p)
 #pragma unroll
-            for (uint32_t q = 0; q < 8; ++q)
+            for (uint32_t q = 0; q < 16; ++q)
                 if (b0 + q < pw && b0 + q < W)
                     rowb[((b0 + q) << 6) + w.lane] = t[q];
         wsync();
@@ -714,6 +745,7 @@ PCG_DEV void op_branch(Wave<LP, I8>& w, uint32_t kind, uint32_t s, uint32_t o, u
     }
     P = np;
     (void)frame_ok;
+    SC_ADD(w.prof, 21, tb2);
 }
 
 template <int LP, bool I8>
@@ -729,6 +761,7 @@ __global__ void __launch_bounds__(64) scl_char_kernel(KernelArgs a, uint32_t Sl)
     w.ly = make_layout(a.N, Sl);
     w.gs = reinterpret_cast<uint32_t*>(a.scratch) + (uint64_t)blockIdx.x * w.ly.gdwords;
     w.lane = threadIdx.x & 63;
+    w.prof = a.prof;
     w.p = w.lane % LP;
     w.gb = w.lane - w.p;
     const uint32_t W = a.N >= 32 ? a.N / 32 : 1u;
@@ -745,10 +778,12 @@ __global__ void __launch_bounds__(64) scl_char_kernel(KernelArgs a, uint32_t Sl)
         w.m = 0;
         w.right = false;
         uint32_t P = 1;
+        SC_T0(tg0);
         for (uint32_t k = 0; k < a.nops; ++k) {
             const uint32_t op = ld_const(a.ops, k);
             const uint32_t code = op_code(op), s = op_stage(op), o = op_off(op);
             const bool act = w.p < P;
+            SC_T0(to0);
             switch (code) {
             case OP_F:
                 op_fg(w, false, s, o, act);
@@ -801,7 +836,10 @@ __global__ void __launch_bounds__(64) scl_char_kernel(KernelArgs a, uint32_t Sl)
                 break;
             }
             wsync();
+            if (code <= OP_COMB || code == OP_CS_R0)
+                SC_ADD(a.prof, code & 63u, to0);
         }
+        SC_T0(tx0);
         // extractBestPath (scl_fip_char.cpp:816-856): first path in list order whose
         // information passes the detector, else path 0
         const bool act = w.p < P;
@@ -847,6 +885,12 @@ __global__ void __launch_bounds__(64) scl_char_kernel(KernelArgs a, uint32_t Sl)
                 a.metrics[frame * a.L + w.p] = act ? (float)w.m : 0.0f;
         }
         wsync();
+        SC_ADD(a.prof, 22, tx0);
+        SC_ADD(a.prof, 61, tg0);
+#ifdef PCG_SCLC_PROF
+        if (a.prof && w.lane == 0)
+            atomicAdd(&a.prof[62], 1ull);
+#endif
     }
 }
 
@@ -870,12 +914,13 @@ uint32_t lp_of(uint32_t L)
 } // namespace
 
 // LDS / scratch layout: stages < Sl in LDS, chosen so a wave's LDS stays within
-// PCG_SCLC_LDS_KB (default 20 KB: 8 waves per CU, measured best at N = 1024, L = 8).
+// PCG_SCLC_LDS_KB (default 12 KB: only the shared small-stage unit in LDS at N = 1024, 14
+// waves per CU -- occupancy beats LDS residency here, measured at N = 1024, L = 8).
 int sclc_layout(uint32_t N, uint32_t L, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratch_dwords)
 {
     if (L < 2 || L > 32 || N < 8)
         return -4;
-    uint32_t budget = 20u * 1024u;
+    uint32_t budget = 12u * 1024u;
     if (const char* e = getenv("PCG_SCLC_LDS_KB"))
         budget = (uint32_t)atoi(e) * 1024u;
     const uint32_t top = (uint32_t)__builtin_ctz(N);
