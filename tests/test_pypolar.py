@@ -85,7 +85,7 @@ def test_mixed_is_adaptive_float():
     with pytest.raises(ValueError):
         pp.PolarDecoder(8, 4, [1, 2, 4], "mixed")
     with pytest.raises(RuntimeError, match="not part of this build"):
-        pp.PolarDecoder(1024, 8, fr, "char")
+        pp.PolarDecoder(1024, 8, fr, "scan")
 
 
 def test_adaptive_plan_host_only():
