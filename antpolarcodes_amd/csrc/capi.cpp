@@ -151,6 +151,14 @@ static int plan_create_impl(pcg_plan** out,
             return fail(rc, "8-bit list decoding layout unsupported for this N/L");
         }
         p->scratch_floats = sd;
+    } else if (L == 1 && p->host.sc_kind == 0) {
+        uint64_t sd = 0;
+        rc = pcg::scs_layout(N, &p->wave_lds_floats, &p->lds_stage_limit, &sd);
+        if (rc != 0) {
+            delete p;
+            return fail(rc, "Fast-SSC layout unsupported for this N");
+        }
+        p->scratch_floats = sd;
     } else if (L == 1) {
         p->wave_lds_floats = pcg::sc_wave_lds_floats(N);
     } else {
@@ -405,6 +413,19 @@ static int decode_impl(pcg_plan* p,
         }
         a.scratch = p->d_scratch;
         rc = pcg::launch_scl_char(a, s);
+    } else if (h.L == 1 && h.sc_kind == 0) {
+        const uint64_t need = pcg::scs_units(F, p->wave_lds_floats);
+        if (p->scratch_floats > 0 && need > p->scratch_frames) {
+            (void)hipFree(p->d_scratch);
+            p->d_scratch = nullptr;
+            p->scratch_frames = 0;
+            hipError_t e = hipMalloc(&p->d_scratch, need * p->scratch_floats * sizeof(float));
+            if (e != hipSuccess)
+                return hip_fail(e, "hipMalloc(scratch)");
+            p->scratch_frames = need;
+        }
+        a.scratch = p->d_scratch;
+        rc = pcg::launch_scs(a, s);
     } else if (h.L == 1) {
         rc = pcg::launch_sc(a, s);
     } else {

@@ -62,4 +62,8 @@ int launch_sclls(const KernelArgs& a, hipStream_t stream);
 // dwords per wave; persistent waves for a launch of F frames
 int sclc_layout(uint32_t N, uint32_t L, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratch_dwords);
 uint64_t sclc_units(uint64_t F, uint32_t L, uint32_t lds_dwords, bool i8);
+// lane-serial Fast-SSC (scs_kernel.hip): layout, persistent waves, launch
+int scs_layout(uint32_t N, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratch_dwords);
+uint64_t scs_units(uint64_t F, uint32_t lds_dwords);
+int launch_scs(const KernelArgs& a, hipStream_t stream);
 } // namespace pcg

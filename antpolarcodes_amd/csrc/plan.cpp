@@ -305,6 +305,10 @@ int build_plan(PlanHost& p,
         const char* k = getenv("PCG_SCL_KERNEL");
         p.scl_kind = (k && std::string(k) == "wave") ? 1 : 0;
     }
+    {
+        const char* k = getenv("PCG_SC_KERNEL"); // dev switch: "wave" = sc_kernel.hip
+        p.sc_kind = (k && std::string(k) == "wave") ? 1 : 0;
+    }
     p.scl_st8 = p.scl_kind == 0 || (L <= 8 && getenv("PCG_SCL_NO_ST8") == nullptr);
     try {
         if (p.fixed && L == 1)

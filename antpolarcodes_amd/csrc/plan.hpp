@@ -93,6 +93,7 @@ struct PlanHost {
     bool scl_st8 = true;            // emit lane-serial size-8 subtrees for SCL
     int scl_kind = 0;               // SCL kernel: 0 lane-serial (sclls_kernel.hip), 1 one codeword per wave
     int fixed = 0;                  // 1: the reference's 8-bit decoders (FastSscFipChar / SclFipChar)
+    int sc_kind = 0;                // Fast-SSC kernel: 0 lane-serial (scs_kernel.hip), 1 one codeword per wave
 };
 
 // Returns 0, or a negative pcg.h error code with *err set.

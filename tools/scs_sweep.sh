@@ -1,0 +1,10 @@
+# lane-serial Fast-SSC: parity (all Fast-SSC GPU tests), then an LDS sweep of the bench
+set -o pipefail
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_sc.py tests/test_gpu_pypolar.py tests/test_gpu_adaptive.py -x -q --timeout 200 --timeout-method thread > gpurun_out/scs_tests.log 2>&1 || { tail -30 gpurun_out/scs_tests.log; exit 1; }
+tail -1 gpurun_out/scs_tests.log
+for kb in ${KBS:-12 16 24 40}; do
+  PCG_SCS_LDS_KB=$kb PCG_DEBUG_OCC=1 timeout -k 10 120 python bench.py --mode sc --no-cpu-baseline > gpurun_out/scs_$kb.json 2> gpurun_out/scs_$kb.err || exit 1
+  echo "kb=$kb $(python -c "import json;d=json.load(open('gpurun_out/scs_$kb.json'));print(round(d['value']/1e6,2),'Mcw/s', round(d['roofline']['kernel_ms'],3),'ms fer', d['frame_error_rate'])") $(grep scs gpurun_out/scs_$kb.err | head -1)"
+done
+PCG_SC_KERNEL=wave timeout -k 10 120 python bench.py --mode sc --no-cpu-baseline > gpurun_out/scs_wave.json 2>/dev/null && echo "wave kernel: $(python -c "import json;d=json.load(open('gpurun_out/scs_wave.json'));print(round(d['value']/1e6,2),'Mcw/s fer', d['frame_error_rate'])")"
