@@ -151,15 +151,12 @@ static int plan_create_impl(pcg_plan** out,
             return fail(rc, "8-bit list decoding layout unsupported for this N/L");
         }
         p->scratch_floats = sd;
-    } else if (L == 1 && p->host.sc_kind == 0) {
-        uint64_t sd = 0;
-        rc = pcg::scs_layout(N, &p->wave_lds_floats, &p->lds_stage_limit, &sd);
-        if (rc != 0) {
-            delete p;
-            return fail(rc, "Fast-SSC layout unsupported for this N");
-        }
-        p->scratch_floats = sd;
+    } else if (L == 1 && p->host.sc_kind == 0 &&
+               pcg::scs_layout(N, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats) == 0) {
+        // lane-serial Fast-SSC (its per-lane bit rows fit the LDS up to N = 8192)
     } else if (L == 1) {
+        p->host.sc_kind = 1; // one codeword per wave (sc_kernel.hip)
+        p->scratch_floats = 0;
         p->wave_lds_floats = pcg::sc_wave_lds_floats(N);
     } else {
         rc = p->host.scl_kind == 0

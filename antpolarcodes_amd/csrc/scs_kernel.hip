@@ -504,21 +504,21 @@ PCG_DEV void inner(Lane& w, uint32_t code, uint32_t s, uint32_t o)
             }
             const uint32_t hq = h / 4;
             uint32_t c = 0;
-            for (; c + 2 <= hq; c += 2) { // two units in flight
-                const float4 a0 = src.ld(c), b0 = src.ld(c + hq), a1 = src.ld(c + 1), b1 = src.ld(c + 1 + hq);
-                if (code == OP_F) {
-                    dst.st(c, f4_f(a0, b0));
-                    dst.st(c + 1, f4_f(a1, b1));
-                } else if (code == OP_G) {
-                    const uint32_t lb = w.bits_at(o + 4u * c, 8);
-                    dst.st(c, f4_g(a0, b0, lb & 0xfu));
-                    dst.st(c + 1, f4_g(a1, b1, lb >> 4));
-                } else {
-                    dst.st(c, f4_add(a0, b0));
-                    dst.st(c + 1, f4_add(a1, b1));
+            for (; c + 4 <= hq; c += 4) { // four units in flight
+                float4 av[4], bv[4];
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    av[q] = src.ld(c + q);
+                    bv[q] = src.ld(c + q + hq);
                 }
+                const uint32_t lb = code == OP_G ? w.bits_at(o + 4u * c, 16) : 0u;
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q)
+                    dst.st(c + q, code == OP_F ? f4_f(av[q], bv[q])
+                                               : (code == OP_G ? f4_g(av[q], bv[q], (lb >> (4u * q)) & 0xfu)
+                                                               : f4_add(av[q], bv[q])));
             }
-            if (c < hq) {
+            for (; c < hq; ++c) {
                 const float4 a0 = src.ld(c), b0 = src.ld(c + hq);
                 dst.st(c, code == OP_F ? f4_f(a0, b0)
                                        : (code == OP_G ? f4_g(a0, b0, w.bits_at(o + 4u * c, 4)) : f4_add(a0, b0)));

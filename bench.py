@@ -225,6 +225,13 @@ def main():
             "frame_error_rate": fer,
             "crc_ok_rate": ok_rate,
         }
+        if world == 1 and punc is None:
+            # PCIe-inclusive rate (host buffers: H2D + decode + D2H, pcg_decode_*_host), never `value`
+            dh = plan.decode_host_i8 if fixed else plan.decode_host
+            dh(llr[:4096])
+            t0 = time.perf_counter()
+            dh(llr)
+            line["host_buffers_cw_per_s"] = F / (time.perf_counter() - t0)
         if not args.no_cpu_baseline and world == 1:
             cpu_llr = llr
             if punc is not None:
