@@ -141,7 +141,12 @@ static int plan_create_impl(pcg_plan** out,
         delete p;
         return fail(rc, err);
     }
-    if (fixed && L == 1) {
+    if (fixed && L == 1 && p->host.sc_kind == 0 &&
+        pcg::sccs_layout(N, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats) == 0) {
+        // lane-serial 8-bit Fast-SSC
+    } else if (fixed && L == 1) {
+        p->host.sc_kind = 1; // one codeword per wave (sc_char_kernel.hip)
+        p->scratch_floats = 0;
         p->wave_lds_floats = pcg::sc_wave_lds_floats(N);
     } else if (fixed) {
         uint64_t sd = 0;
@@ -395,7 +400,20 @@ static int decode_impl(pcg_plan* p,
         a.flags = (uint32_t)strtoul(fl, nullptr, 0);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     int rc;
-    if (h.fixed && h.L == 1) {
+    if (h.fixed && h.L == 1 && h.sc_kind == 0) {
+        const uint64_t need = pcg::sccs_units(F, p->wave_lds_floats, llr8 != nullptr);
+        if (p->scratch_floats > 0 && need > p->scratch_frames) {
+            (void)hipFree(p->d_scratch);
+            p->d_scratch = nullptr;
+            p->scratch_frames = 0;
+            hipError_t e = hipMalloc(&p->d_scratch, need * p->scratch_floats * sizeof(uint32_t));
+            if (e != hipSuccess)
+                return hip_fail(e, "hipMalloc(scratch)");
+            p->scratch_frames = need;
+        }
+        a.scratch = p->d_scratch;
+        rc = pcg::launch_sccs(a, s);
+    } else if (h.fixed && h.L == 1) {
         rc = pcg::launch_sc_char(a, s);
     } else if (h.fixed) {
         const uint64_t need = pcg::sclc_units(F, h.L, p->wave_lds_floats, llr8 != nullptr);

@@ -66,4 +66,8 @@ uint64_t sclc_units(uint64_t F, uint32_t L, uint32_t lds_dwords, bool i8);
 int scs_layout(uint32_t N, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratch_dwords);
 uint64_t scs_units(uint64_t F, uint32_t lds_dwords);
 int launch_scs(const KernelArgs& a, hipStream_t stream);
+// lane-serial 8-bit Fast-SSC (sccs_kernel.hip)
+int sccs_layout(uint32_t N, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratch_dwords);
+uint64_t sccs_units(uint64_t F, uint32_t lds_dwords, bool i8);
+int launch_sccs(const KernelArgs& a, hipStream_t stream);
 } // namespace pcg
