@@ -182,3 +182,27 @@ def test_torch_device_path_i8(oracle):
     torch.cuda.synchronize()
     oi, ook = oracle.sclc_decode(N, L, fr, x8, crc=8)
     assert np.array_equal(info.cpu().numpy(), oi) and np.array_equal(ok.cpu().numpy(), ook)
+
+
+@pytest.mark.parametrize("F", [1, 63, 65, 1000])
+def test_scc_lane_serial_batch_edges(oracle, F):
+    rng = np.random.default_rng(F)
+    _check(oracle, 256, 1, frozen_bits(256, 128, 0.0), i8_kinds(rng, F, 256, "sat"))
+
+
+def test_scc_wave_kernel_switch(oracle, monkeypatch):
+    """The one-codeword-per-wave 8-bit kernel (PCG_SC_KERNEL=wave) stays bit-exact."""
+    monkeypatch.setenv("PCG_SC_KERNEL", "wave")
+    rng = np.random.default_rng(5)
+    for N in (32, 256, 1024):
+        _check(oracle, N, 1, frozen_bits(N, N // 2, 0.0), i8_kinds(rng, 64, N, "normal"))
+
+
+def test_sclc_layout_variants(oracle, monkeypatch):
+    """Every stage placement (LDS budget) of the 8-bit SCL kernel decodes identically."""
+    rng = np.random.default_rng(9)
+    fr = frozen_bits(1024, 512, 0.0)
+    x8 = i8_kinds(rng, 64, 1024, "normal")
+    for kb in ("12", "20", "40", "80"):
+        monkeypatch.setenv("PCG_SCLC_LDS_KB", kb)
+        _check(oracle, 1024, 8, fr, x8)

@@ -109,3 +109,28 @@ def test_sc_device_path_torch(oracle):
     oi, ook = oracle.sc_decode(1024, fr, llr)
     assert np.array_equal(d_info.cpu().numpy(), oi)
     assert np.array_equal(d_ok.cpu().numpy(), ook)
+
+
+@pytest.mark.parametrize("N", [8192, 16384])
+def test_sc_large_blocks(oracle, N):
+    """Lane-serial Fast-SSC with large per-lane bit rows (64 KB / 128 KB of LDS per wave)."""
+    rng = np.random.default_rng(N)
+    fr = _bb(oracle, N, N // 2)
+    _check_sc(oracle, N, fr, llr_kinds(rng, 70, N, "normal"))
+
+
+@pytest.mark.parametrize("F", [1, 63, 64, 65, 129, 1000])
+def test_sc_batch_edges(oracle, F):
+    """Partial last wave of the lane-serial kernel (64 frames per wave)."""
+    rng = np.random.default_rng(F)
+    fr = _bb(oracle, 1024, 512)
+    _check_sc(oracle, 1024, fr, llr_kinds(rng, F, 1024, "zeros"))
+
+
+def test_sc_wave_kernel_switch(oracle, monkeypatch):
+    """The one-codeword-per-wave kernel (dev switch PCG_SC_KERNEL=wave) stays bit-exact."""
+    monkeypatch.setenv("PCG_SC_KERNEL", "wave")
+    rng = np.random.default_rng(3)
+    for N, K in ((64, 32), (1024, 512)):
+        fr = _bb(oracle, N, K)
+        _check_sc(oracle, N, fr, llr_kinds(rng, 100, N, "ints"))
