@@ -73,6 +73,7 @@ def lib():
         L.pcg_plan_create.argtypes = [C.POINTER(P), C.c_uint32, C.c_uint32, P, C.c_uint32, C.c_int, C.c_int, C.c_int]
         L.pcg_plan_create_adaptive.argtypes = L.pcg_plan_create.argtypes
         L.pcg_plan_create_char.argtypes = L.pcg_plan_create.argtypes
+        L.pcg_plan_create_adaptive_char.argtypes = L.pcg_plan_create.argtypes
         L.pcg_decode_i8.argtypes = [P, P, C.c_uint64, P, P, P, P]
         L.pcg_decode_i8_host.argtypes = [P, P, C.c_uint64, P, P, P]
         L.pcg_decode_f32.argtypes = [P, P, C.c_uint64, P, P, P, P]
@@ -133,13 +134,13 @@ class Plan:
     def __init__(self, N, L, frozen, systematic=True, crc=8, device=0, adaptive=False, fixed=False):
         """adaptive=True: Fast-SSC first, SCL-L for the frames whose check fails
         (AdaptiveFloat, pcg_plan_create_adaptive).  fixed=True: the reference's 8-bit
-        decoders FastSscFipChar / SclFipChar (pcg_plan_create_char)."""
+        decoders FastSscFipChar / SclFipChar (pcg_plan_create_char); both: AdaptiveChar."""
         fr = np.ascontiguousarray(np.asarray(list(frozen), dtype=np.uint32))
         h = C.c_void_p()
-        if adaptive and fixed:
-            raise ValueError("the adaptive decoder is float only (AdaptiveFloat)")
-        create = (lib().pcg_plan_create_adaptive if adaptive else
-                  lib().pcg_plan_create_char if fixed else lib().pcg_plan_create)
+        if adaptive:  # AdaptiveFloat / AdaptiveChar
+            create = lib().pcg_plan_create_adaptive_char if fixed else lib().pcg_plan_create_adaptive
+        else:
+            create = lib().pcg_plan_create_char if fixed else lib().pcg_plan_create
         _check(create(C.byref(h), int(N), int(L), fr.ctypes.data if fr.size else None,
                       int(fr.size), int(bool(systematic)), int(crc), int(device)))
         self._h = h

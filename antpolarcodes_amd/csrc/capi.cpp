@@ -242,6 +242,39 @@ int pcg_plan_create_char(pcg_plan** out,
     return plan_create_impl(out, N, L, frozen, n_frozen, systematic, crc_kind, device, 1);
 }
 
+static int plan_create_adaptive_impl(pcg_plan** out,
+                                     uint32_t N,
+                                     uint32_t L,
+                                     const uint32_t* frozen,
+                                     uint32_t n_frozen,
+                                     int systematic,
+                                     int crc_kind,
+                                     int device,
+                                     int fixed)
+{
+    if (L < 2) // makeDecoder with listSize 1 builds the plain Fast-SSC decoder (decoder.cpp:60-68)
+        return plan_create_impl(out, N, L, frozen, n_frozen, systematic, crc_kind, device, fixed);
+    int rc = plan_create_impl(out, N, L, frozen, n_frozen, systematic, crc_kind, device, fixed);
+    if (rc != 0)
+        return rc;
+    if (!fixed && (*out)->host.scl_kind != 0) {
+        pcg_plan_destroy(*out);
+        *out = nullptr;
+        return fail(PCG_E_UNSUPPORTED, "adaptive decoding needs the lane-serial SCL kernel");
+    }
+    pcg_plan* fast = nullptr;
+    // the Fast-SSC stage rejects what its constructor rejects (invalid_argument)
+    rc = plan_create_impl(&fast, N, 1, frozen, n_frozen, systematic, crc_kind, device, fixed);
+    if (rc != 0) {
+        std::string msg = g_last_error;
+        pcg_plan_destroy(*out);
+        *out = nullptr;
+        return fail(rc, msg);
+    }
+    (*out)->fast = fast;
+    return PCG_OK;
+}
+
 int pcg_plan_create_adaptive(pcg_plan** out,
                              uint32_t N,
                              uint32_t L,
@@ -251,27 +284,19 @@ int pcg_plan_create_adaptive(pcg_plan** out,
                              int crc_kind,
                              int device)
 {
-    if (L < 2) // makeDecoder with listSize 1 builds the plain Fast-SSC decoder (decoder.cpp:60-68)
-        return pcg_plan_create(out, N, L, frozen, n_frozen, systematic, crc_kind, device);
-    int rc = pcg_plan_create(out, N, L, frozen, n_frozen, systematic, crc_kind, device);
-    if (rc != 0)
-        return rc;
-    if ((*out)->host.scl_kind != 0) {
-        pcg_plan_destroy(*out);
-        *out = nullptr;
-        return fail(PCG_E_UNSUPPORTED, "adaptive decoding needs the lane-serial SCL kernel");
-    }
-    pcg_plan* fast = nullptr;
-    // the Fast-SSC stage rejects what FastSscAvxFloat's constructor rejects (invalid_argument)
-    rc = pcg_plan_create(&fast, N, 1, frozen, n_frozen, systematic, crc_kind, device);
-    if (rc != 0) {
-        std::string msg = g_last_error;
-        pcg_plan_destroy(*out);
-        *out = nullptr;
-        return fail(rc, msg);
-    }
-    (*out)->fast = fast;
-    return PCG_OK;
+    return plan_create_adaptive_impl(out, N, L, frozen, n_frozen, systematic, crc_kind, device, 0);
+}
+
+int pcg_plan_create_adaptive_char(pcg_plan** out,
+                                  uint32_t N,
+                                  uint32_t L,
+                                  const uint32_t* frozen,
+                                  uint32_t n_frozen,
+                                  int systematic,
+                                  int crc_kind,
+                                  int device)
+{
+    return plan_create_adaptive_impl(out, N, L, frozen, n_frozen, systematic, crc_kind, device, 1);
 }
 
 int pcg_plan_describe(const pcg_plan* p, pcg_plan_desc* d)
@@ -302,7 +327,7 @@ static int decode_impl(pcg_plan* p,
                        const int8_t* llr8 = nullptr);
 
 static int decode_adaptive(pcg_plan* p, const float* llr, uint64_t F, uint8_t* info, uint8_t* ok, float* metrics,
-                           void* stream)
+                           void* stream, const int8_t* llr8 = nullptr)
 {
     // AdaptiveFloat::decode (adaptive_float.cpp:33-45): Fast-SSC for every frame, then SCL
     // for the frames whose check failed, whose SCL output (and ok) replaces the SC one.
@@ -319,14 +344,14 @@ static int decode_adaptive(pcg_plan* p, const float* llr, uint64_t F, uint8_t* i
         p->fmap_frames = F;
     }
     uint8_t* okb = ok ? ok : p->d_okbuf;
-    int rc = decode_impl(p->fast, llr, F, info, okb, nullptr, stream, nullptr, nullptr);
+    int rc = decode_impl(p->fast, llr, F, info, okb, nullptr, stream, nullptr, nullptr, llr8);
     if (rc != 0)
         return rc;
     if (metrics && (e = hipMemsetAsync(metrics, 0, F * p->host.L * sizeof(float), s)) != hipSuccess)
         return hip_fail(e, "hipMemsetAsync(metrics)");
     if (pcg::launch_compact_failed(okb, F, p->d_fmap + 1, p->d_fmap, s) != 0)
         return fail(PCG_E_HIP, std::string("compaction launch failed: ") + hipGetErrorString(hipGetLastError()));
-    return decode_impl(p, llr, F, info, okb, metrics, stream, p->d_fmap + 1, p->d_fmap);
+    return decode_impl(p, llr, F, info, okb, metrics, stream, p->d_fmap + 1, p->d_fmap, llr8);
 }
 
 int pcg_decode_f32(pcg_plan* p,
@@ -486,6 +511,8 @@ int pcg_decode_i8(pcg_plan* p,
     if (F > 0xFFFFFFFFull)
         return fail(PCG_E_ARG, "at most 2^32 - 1 frames per call");
     DeviceGuard g(p->device);
+    if (p->fast)
+        return decode_adaptive(p, nullptr, F, info, ok, metrics, stream, llr);
     return decode_impl(p, nullptr, F, info, ok, metrics, stream, nullptr, nullptr, llr);
 }
 

@@ -420,9 +420,9 @@ void GpuDecoder::initialize(size_t blockLength, const std::vector<unsigned>& fro
     if (rc != 0)
         throw_pcg(rc);
     pcg_plan_destroy(probe);
-    if (mAdaptive) { // AdaptiveFloat also constructs a FastSscAvxFloat (adaptive_float.cpp:23)
-        rc = pcg_plan_create(&probe, (uint32_t)blockLength, 1, mFrozenBits.data(), (uint32_t)mFrozenBits.size(), 1,
-                             0, -1);
+    if (mAdaptive) { // AdaptiveFloat / AdaptiveChar also construct their Fast-SSC decoder
+        rc = (mFixed ? pcg_plan_create_char : pcg_plan_create)(&probe, (uint32_t)blockLength, 1, mFrozenBits.data(),
+                                                               (uint32_t)mFrozenBits.size(), 1, 0, -1);
         if (rc != 0)
             throw_pcg(rc);
         pcg_plan_destroy(probe);
@@ -444,7 +444,8 @@ void GpuDecoder::ensurePlan()
     if (mPlan && kind == mPlanKind && mSystematic == mPlanSys)
         return;
     releasePlan();
-    auto create = mAdaptive ? pcg_plan_create_adaptive : (mFixed ? pcg_plan_create_char : pcg_plan_create);
+    auto create = mAdaptive ? (mFixed ? pcg_plan_create_adaptive_char : pcg_plan_create_adaptive)
+                            : (mFixed ? pcg_plan_create_char : pcg_plan_create);
     const int rc = create(&mPlan, (uint32_t)mBlockLength, (uint32_t)mListSize, mFrozenBits.data(),
                           (uint32_t)mFrozenBits.size(), mSystematic ? 1 : 0, kind, mDevice);
     if (rc != 0) {
@@ -546,6 +547,15 @@ GpuFastSscChar::GpuFastSscChar(size_t blockLength, const std::vector<unsigned>& 
 GpuSclChar::GpuSclChar(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits, int device)
     : GpuDecoder(blockLength, listSize, {}, device)
 {
+    mFixed = true;
+    initialize(blockLength, frozenBits);
+}
+
+GpuAdaptiveChar::GpuAdaptiveChar(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,
+                                 int device)
+    : GpuDecoder(blockLength, listSize, {}, device)
+{
+    mAdaptive = true;
     mFixed = true;
     initialize(blockLength, frozenBits);
 }

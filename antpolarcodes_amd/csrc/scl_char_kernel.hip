@@ -536,15 +536,18 @@ __global__ void __launch_bounds__(64) scl_char_kernel(KernelArgs a, uint32_t Sl)
     w.p = w.lane % LP;
     w.gb = w.lane - w.p;
     const uint32_t W = a.N >= 32 ? a.N / 32 : 1u;
-    const uint64_t ngroups = (a.F + G - 1) / G;
+    // frames 0 .. F-1, or fmap[0 .. *fcount) (the adaptive decoder's second stage)
+    const uint64_t Fn = a.fcount ? (uint64_t)*a.fcount : a.F;
+    const uint64_t ngroups = (Fn + G - 1) / G;
     for (uint64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
-        const uint64_t frame = grp * G + w.lane / LP;
-        const bool fok = frame < a.F;
-        const uint64_t fr = fok ? frame : a.F - 1;
+        const uint64_t slot = grp * G + w.lane / LP;
+        const bool fok = slot < Fn;
+        const uint64_t fs = fok ? slot : Fn - 1;
+        const uint64_t frame = a.fmap ? (uint64_t)a.fmap[fs] : fs;
         if constexpr (I8)
-            w.chan = a.llr8 + fr * a.N;
+            w.chan = a.llr8 + frame * a.N;
         else
-            w.chan = a.llr + fr * a.N;
+            w.chan = a.llr + frame * a.N;
         w.ptr = 0;
         w.m = 0;
         w.right = false;

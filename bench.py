@@ -9,7 +9,7 @@ rank decodes its own batch (independent frames shard with no collective:
 weak scaling); the barrier/max-reduction uses gloo on the host.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-                       [--mode scl8|sc|scl32|nr5g|adaptive8|sc_char|scl8_char]
+                       [--mode scl8|sc|scl32|nr5g|adaptive8|sc_char|scl8_char|adaptive8_char]
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -34,6 +34,9 @@ MODES = {
                                        "(amplification 10, pcsim's amp-fixed), N=1024 K=512, 2^16 frames"),
     "scl8_char": (1024, 512, 8, 1 << 16, "config 3 through the 8-bit decoder (SclFipChar): int8 LLRs "
                                          "(amplification 10, pcsim's amp-fixed), N=1024 K=512, 2^16 frames"),
+    "adaptive8_char": (1024, 512, 8, 1 << 16, "config 3 with pcsim's 8-bit list decoder (AdaptiveChar): "
+                                              "FastSscFipChar, then SclFipChar L=8 for CRC-8 failures, int8 LLRs "
+                                              "(amplification 10), N=1024 K=512, 2^16 frames"),
 }
 CHAR_AMP = 10.0  # src/simulation/setup.cpp:58 "amp-fixed" (8-bit pre-quantisation scaling)
 NR_E = 896
@@ -132,10 +135,10 @@ def main():
         frozen = frozen_bits(N, K, 0.0, "BB")
         llr, info, _ = frames.awgn_frames(N, frozen, F, args.ebn0, seed=1000 + rank, crc=crc)
     fixed = args.mode.endswith("_char")
+    adaptive = args.mode.startswith("adaptive")
     if fixed:  # pcsim's Scale(amplification) then CharContainer::insertLlr (host side, once)
         llr = np.clip(np.rint(llr * CHAR_AMP), -128, 127).astype(np.int8)
-    plan = Plan(N, L, frozen, systematic=True, crc=crc, device=local, adaptive=args.mode == "adaptive8",
-                fixed=fixed)
+    plan = Plan(N, L, frozen, systematic=True, crc=crc, device=local, adaptive=adaptive, fixed=fixed)
     kb = plan.kb
     d_llr = torch.from_numpy(llr).to(f"cuda:{local}")
     d_info = torch.empty((F, kb), dtype=torch.uint8, device=f"cuda:{local}")

@@ -26,6 +26,7 @@
  *   pcg_decode_i8     <- Decoder::decode_vector(const char*, void*) decoder.cpp:169-181,
  *                        batched, device-resident int8 LLRs
  *   pcg_decode_i8_host <- the same with host buffers
+ *   pcg_plan_create_adaptive_char <- AdaptiveChar, adaptive_char.cpp:14-45
  *   pcg_plan_destroy  <- Decoder::~Decoder decoder.cpp:104-114
  *   pcg_last_error    <- the std::exception text the reference throws
  *   pcg_puncturer_*   <- PolarCode::Puncturer (include/polarcode/puncturer.h:33-99,
@@ -154,6 +155,18 @@ int pcg_plan_create_char(pcg_plan** plan,
                          int systematic,
                          int crc_kind,
                          int device);
+
+/* The 8-bit adaptive decoder AdaptiveChar (adaptive_char.cpp:14-45; pcsim's 8-bit list
+ * decoding, simulator.cpp:722-727): FastSscFipChar for every frame, SclFipChar for the
+ * frames whose check failed, as pcg_plan_create_adaptive does for the float decoders. */
+int pcg_plan_create_adaptive_char(pcg_plan** plan,
+                                  uint32_t N,
+                                  uint32_t L,
+                                  const uint32_t* frozen,
+                                  uint32_t n_frozen,
+                                  int systematic,
+                                  int crc_kind,
+                                  int device);
 
 /* Decode F frames of int8 LLRs (device pointer, F x N bytes) with an 8-bit plan; outputs
  * as pcg_decode_f32.  PCG_E_ARG for a float plan.  Asynchronous. */

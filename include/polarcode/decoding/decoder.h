@@ -165,6 +165,15 @@ public:
     GpuSclChar(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits, int device = 0);
 };
 
+/// AdaptiveChar (adaptive_char.cpp:14-45; pcsim's 8-bit list decoding): FastSscFipChar, then
+/// SclFipChar for the frames whose check fails.  Not reachable through create(), as in the reference.
+class GpuAdaptiveChar : public GpuDecoder
+{
+public:
+    GpuAdaptiveChar(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,
+                    int device = 0);
+};
+
 /// decoder_impl as in decoder.cpp:54-87: 0 = char (FastSscFipChar / SclFipChar), 1 = float
 /// (Fast-SSC / SCL), 2 = AdaptiveFloat (list size >= 2); SCAN (3) is not part of this build.
 Decoder* makeDecoder(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,

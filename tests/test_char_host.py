@@ -74,3 +74,13 @@ def test_pypolar_char_factory_without_gpu():
         pypolar.PolarDecoder(256, 4, fr, "scan")
     with pytest.raises(Exception, match="Unknown PolarDecoder type"):
         pypolar.PolarDecoder(256, 4, fr, "bogus")
+
+
+def test_adaptive_char_plan_host_only():
+    """AdaptiveChar (adaptive_char.cpp:14-45) builds both 8-bit stages; L < 2 is plain
+    FastSscFipChar (makeDecoder's listSize-1 branch)."""
+    nat = _nat()
+    fr = frozen_bits(256, 128, 0.0)
+    d = nat.Plan(256, 8, fr, adaptive=True, fixed=True, device=-1).describe()
+    assert d["list_size"] == 8
+    assert nat.Plan(256, 1, fr, adaptive=True, fixed=True, device=-1).describe()["list_size"] == 1

@@ -206,3 +206,23 @@ def test_sclc_layout_variants(oracle, monkeypatch):
     for kb in ("12", "20", "40", "80"):
         monkeypatch.setenv("PCG_SCLC_LDS_KB", kb)
         _check(oracle, 1024, 8, fr, x8)
+
+
+@pytest.mark.parametrize("crc", [8, 16])
+def test_adaptive_char_matches_oracle(oracle, crc):
+    """AdaptiveChar (adaptive_char.cpp:33-45): FastSscFipChar, SclFipChar for the failures."""
+    from antpolarcodes_amd._native import Plan
+    N, L = 1024, 8
+    fr = frozen_bits(N, 512, 0.0)
+    llr, _, _ = frames.awgn_frames(N, fr, 3000, 1.5, seed=crc, crc=crc)
+    x8 = np.clip(np.rint(llr * 10.0), -128, 127).astype(np.int8)
+    si, sok = oracle.scc_decode(N, fr, x8, crc=crc)
+    li, lok = oracle.sclc_decode(N, L, fr, x8, crc=crc)
+    exp = np.where(sok[:, None] == 1, si, li)
+    eok = np.where(sok == 1, sok, lok)
+    assert (sok == 0).sum() > 10  # the list stage runs
+    p = Plan(N, L, fr, crc=crc, device=0, fixed=True, adaptive=True)
+    gi, gok, _ = p.decode_host_i8(x8)
+    assert np.array_equal(gi, exp) and np.array_equal(gok, eok)
+    gi, gok, _ = p.decode_host(llr * 10.0)  # float frames, quantised in the kernels
+    assert np.array_equal(gi, exp) and np.array_equal(gok, eok)
