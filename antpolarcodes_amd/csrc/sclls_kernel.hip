@@ -1354,6 +1354,10 @@ uint64_t sclls_units(uint64_t F, uint32_t L, uint32_t wave_lds_floats)
     uint64_t wpc = res > 0 ? (uint64_t)res : 1;
     if (wpc > 8)
         wpc = 8;
+    // L = 32 (N = 4096: 5 resident waves/CU, SIMDs at 2-1-1-1): oversubscribe so the
+    // dispatcher balances groups across SIMDs (measured 3.27e5 -> 4.11e5 cw/s at 32/CU)
+    if (lp_of(L) == 32)
+        wpc = 32;
     if (const char* e = getenv("PCG_SCL_WPC"))
         wpc = (uint64_t)atoi(e);
     if (getenv("PCG_DEBUG_OCC"))
