@@ -79,6 +79,9 @@ def lib():
         L.pcg_decode_f32.argtypes = [P, P, C.c_uint64, P, P, P, P]
         L.pcg_decode_f32_host.argtypes = [P, P, C.c_uint64, P, P, P]
         L.pcg_plan_describe.argtypes = [P, C.POINTER(PlanDesc)]
+        L.pcg_plan_kernel_name.argtypes = [P]
+        L.pcg_plan_kernel_name.restype = C.c_char_p
+        L.pcg_plan_set_initial_metric.argtypes = [P, C.c_float]
         L.pcg_plan_destroy.argtypes = [P]
         L.pcg_plan_destroy.restype = None
         L.pcg_last_error.restype = C.c_char_p
@@ -116,6 +119,24 @@ def _ptr(t):
     return t if isinstance(t, int) else t.data_ptr()
 
 
+def _check_tensor(name, t, dtype, shape, device):
+    """Device-buffer arguments of the decode calls: a torch tensor must have the plan's
+    dtype, exact shape, be contiguous and live on the plan's device (a mismatch would let
+    the kernel read or write out of bounds); raw integer pointers are taken as given."""
+    if t is None or isinstance(t, int):
+        return
+    import torch
+    if t.dtype != dtype:
+        raise ValueError(f"{name}: dtype {t.dtype}, expected {dtype}")
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: shape {tuple(t.shape)}, expected {tuple(shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: tensor must be contiguous")
+    if t.device.type != "cuda" or (t.device.index if t.device.index is not None else torch.cuda.current_device()) \
+            != device:
+        raise ValueError(f"{name}: on {t.device}, the plan lives on cuda:{device}")
+
+
 def _stream(stream, t):
     if stream is not None:
         return stream
@@ -149,6 +170,25 @@ class Plan:
         self.device = device
         self.fixed = bool(fixed)
 
+    def kernel_name(self):
+        """The decode kernel as rocprofv3 names it (pcg_plan_kernel_name)."""
+        return lib().pcg_plan_kernel_name(self._h).decode()
+
+    def set_initial_metric(self, m):
+        """SCL: initial path-0 metric of later decodes (reference metric carry)."""
+        _check(lib().pcg_plan_set_initial_metric(self._h, float(m)))
+
+    def _check_io(self, llr, info, ok, metrics, dtype):
+        import torch
+        F = llr.shape[0] if hasattr(llr, "shape") else None
+        if F is None:
+            raise ValueError("llr must be a tensor (its first dimension is the frame count)")
+        _check_tensor("llr", llr, dtype, (F, self.N), self.device)
+        _check_tensor("info", info, torch.uint8, (F, self.kb), self.device)
+        _check_tensor("ok", ok, torch.uint8, (F,), self.device)
+        _check_tensor("metrics", metrics, torch.float32, (F, self.L), self.device)
+        return F
+
     def describe(self):
         d = PlanDesc()
         _check(lib().pcg_plan_describe(self._h, C.byref(d)))
@@ -178,24 +218,28 @@ class Plan:
         return info, ok, met
 
     def decode_device_i8(self, llr, info, ok=None, metrics=None, stream=None):
-        """int8 device frames (torch.int8 tensors or raw pointers): pcg_decode_i8."""
-        _check(lib().pcg_decode_i8(self._h, _ptr(llr), llr.shape[0], _ptr(info), _ptr(ok), _ptr(metrics),
+        """int8 device frames (torch.int8 CUDA tensors F x N): pcg_decode_i8."""
+        import torch
+        F = self._check_io(llr, info, ok, metrics, torch.int8)
+        _check(lib().pcg_decode_i8(self._h, _ptr(llr), F, _ptr(info), _ptr(ok), _ptr(metrics),
                                    _stream(stream, llr)))
 
     def decode_device(self, llr, info, ok=None, metrics=None, stream=None):
-        """Device-resident decode; arguments are torch CUDA tensors (or raw ints)."""
-        def ptr(t):
-            if t is None:
-                return None
-            return t if isinstance(t, int) else t.data_ptr()
-        F = llr.shape[0] if hasattr(llr, "shape") else None
-        if stream is None:
-            import torch
-            stream = torch.cuda.current_stream(llr.device).cuda_stream
-        _check(lib().pcg_decode_f32(self._h, ptr(llr), F, ptr(info), ptr(ok), ptr(metrics), stream))
+        """Device-resident decode of torch CUDA tensors: llr float32 F x N, info uint8
+        F x ceil(K/8), ok uint8 F (or None), metrics float32 F x L (or None)."""
+        import torch
+        F = self._check_io(llr, info, ok, metrics, torch.float32)
+        _check(lib().pcg_decode_f32(self._h, _ptr(llr), F, _ptr(info), _ptr(ok), _ptr(metrics),
+                                    _stream(stream, llr)))
 
     def decode_punctured_device(self, punc, llr, info, ok=None, metrics=None, stream=None):
         """Depuncture (F x E, device) with `punc` and decode, one stream-ordered call."""
+        import torch
+        F = llr.shape[0]
+        _check_tensor("llr", llr, torch.float32, (F, punc.E), self.device)
+        _check_tensor("info", info, torch.uint8, (F, self.kb), self.device)
+        _check_tensor("ok", ok, torch.uint8, (F,), self.device)
+        _check_tensor("metrics", metrics, torch.float32, (F, self.L), self.device)
         _check(lib().pcg_decode_punctured_f32(self._h, punc._h, _ptr(llr), llr.shape[0], _ptr(info), _ptr(ok),
                                               _ptr(metrics), _stream(stream, llr)))
 

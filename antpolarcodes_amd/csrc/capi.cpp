@@ -21,9 +21,19 @@ struct pcg_plan {
     uint32_t wave_lds_floats = 0;
     uint32_t lds_stage_limit = 0;
     uint32_t scl_virt = 0;
-    uint64_t scratch_floats = 0;  // per scratch unit (codeword or lane-serial wave)
-    float* d_scratch = nullptr;   // grown on demand
+    uint64_t scratch_floats = 0;  // per scratch unit (lane-serial wave)
+    float* d_scratch = nullptr;   // grown stream-ordered (hipMallocAsync) when a launch needs more waves
     uint64_t scratch_frames = 0;  // capacity in scratch units
+    // persistent-wave caps of this plan's kernel on its device (float / int8 channel input),
+    // evaluated once at plan creation
+    uint64_t wave_cap = 0;
+    uint64_t wave_cap_i8 = 0;
+    uint32_t* d_queue = nullptr;  // lane-serial SCL work queue: two zeroed counters
+    const char* kernel = "";      // name of the decode kernel (pcg_plan_kernel_name)
+    // developer switches, read from the environment once at plan creation
+    uint32_t dev_flags = 0;
+    bool dev_opprof = false;
+    float metric0 = 0.0f;         // initial path-0 metric (pcg_plan_set_initial_metric)
     // host-pointer path staging
     float* d_llr = nullptr;
     uint8_t* d_info = nullptr;
@@ -77,7 +87,11 @@ void free_plan_device(pcg_plan* p)
     (void)hipFree(p->d_ops);
     (void)hipFree(p->d_info_pos);
     (void)hipFree(p->d_crc_m);
-    (void)hipFree(p->d_scratch);
+    if (p->d_scratch) { // stream-ordered allocation: free it in order, then wait
+        (void)hipFreeAsync(p->d_scratch, nullptr);
+        (void)hipStreamSynchronize(nullptr);
+    }
+    (void)hipFree(p->d_queue);
     (void)hipFree(p->d_llr);
     (void)hipFree(p->d_info);
     (void)hipFree(p->d_ok);
@@ -85,6 +99,48 @@ void free_plan_device(pcg_plan* p)
     (void)hipFree(p->d_dep);
     (void)hipFree(p->d_fmap);
     (void)hipFree(p->d_okbuf);
+}
+
+// LP: the list size rounded up to a power of two (>= 2), the lane-serial kernels' template
+uint32_t list_pow2(uint32_t L)
+{
+    uint32_t lp = 2;
+    while (lp < L)
+        lp <<= 1;
+    return lp;
+}
+
+const char* kernel_name(const pcg::PlanHost& h)
+{
+    static const char* const sclls[] = {"sclls_kernel<2>", "sclls_kernel<4>", "sclls_kernel<8>",
+                                        "sclls_kernel<16>", "sclls_kernel<32>"};
+    static const char* const sclc[] = {"scl_char_kernel<2>", "scl_char_kernel<4>", "scl_char_kernel<8>",
+                                       "scl_char_kernel<16>", "scl_char_kernel<32>"};
+    if (h.L == 1) {
+        if (h.fixed)
+            return h.sc_kind == 0 ? "sccs_kernel" : "sc_char_kernel";
+        return h.sc_kind == 0 ? "scs_kernel" : "sc_kernel";
+    }
+    const int i = __builtin_ctz(list_pow2(h.L)) - 1;
+    return h.fixed ? sclc[i] : sclls[i];
+}
+
+// Grow the plan's scratch to `units` waves, in stream order (no device-wide sync).
+int grow_scratch(pcg_plan* p, uint64_t units, size_t elem, hipStream_t s)
+{
+    if (p->scratch_floats == 0 || units <= p->scratch_frames)
+        return PCG_OK;
+    if (p->d_scratch)
+        (void)hipFreeAsync(p->d_scratch, s);
+    p->d_scratch = nullptr;
+    p->scratch_frames = 0;
+    void* ptr = nullptr;
+    hipError_t e = hipMallocAsync(&ptr, units * p->scratch_floats * elem, s);
+    if (e != hipSuccess)
+        return hip_fail(e, "hipMallocAsync(scratch)");
+    p->d_scratch = static_cast<float*>(ptr);
+    p->scratch_frames = units;
+    return PCG_OK;
 }
 
 } // namespace
@@ -164,14 +220,16 @@ static int plan_create_impl(pcg_plan** out,
         p->scratch_floats = 0;
         p->wave_lds_floats = pcg::sc_wave_lds_floats(N);
     } else {
-        rc = p->host.scl_kind == 0
-                 ? pcg::sclls_layout(N, L, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats, &p->scl_virt)
-                 : pcg::scl_layout(N, L, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats);
+        rc = pcg::sclls_layout(N, L, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats, &p->scl_virt);
         if (rc != 0) {
             delete p;
             return fail(rc, "list decoding layout unsupported for this N/L");
         }
     }
+    p->kernel = kernel_name(p->host);
+    p->dev_opprof = getenv("PCG_OPPROF") != nullptr;
+    if (const char* fl = getenv("PCG_FLAGS"))
+        p->dev_flags = (uint32_t)strtoul(fl, nullptr, 0);
     if (device < 0) { // host-only plan: classification / validation without a GPU
         p->device = -1;
         *out = p;
@@ -200,6 +258,27 @@ static int plan_create_impl(pcg_plan** out,
         free_plan_device(p);
         delete p;
         return hip_fail(e, "hipMalloc(plan)");
+    }
+    // wave caps (hipOccupancy) of the lane-serial kernels, once per plan
+    if (h.fixed && h.L == 1 && h.sc_kind == 0) {
+        p->wave_cap = pcg::sccs_wave_cap(p->wave_lds_floats, false);
+        p->wave_cap_i8 = pcg::sccs_wave_cap(p->wave_lds_floats, true);
+    } else if (h.fixed && h.L > 1) {
+        p->wave_cap = pcg::sclc_wave_cap(h.L, p->wave_lds_floats, false);
+        p->wave_cap_i8 = pcg::sclc_wave_cap(h.L, p->wave_lds_floats, true);
+    } else if (!h.fixed && h.L == 1 && h.sc_kind == 0) {
+        p->wave_cap = pcg::scs_wave_cap(p->wave_lds_floats);
+    } else if (!h.fixed && h.L > 1) {
+        p->wave_cap = pcg::sclls_wave_cap(h.L, p->wave_lds_floats);
+        const char* q = getenv("PCG_SCL_QUEUE"); // dev switch: 0 = static grid stride
+        if (!(q && q[0] == '0')) {
+            if ((e = hipMalloc(&p->d_queue, 2 * sizeof(uint32_t))) != hipSuccess ||
+                (e = hipMemset(p->d_queue, 0, 2 * sizeof(uint32_t))) != hipSuccess) {
+                free_plan_device(p);
+                delete p;
+                return hip_fail(e, "hipMalloc(work queue)");
+            }
+        }
     }
     if ((e = hipMemcpy(p->d_ops, h.ops.data(), 4 * h.ops.size(), hipMemcpyHostToDevice)) != hipSuccess ||
         (!h.info_pos.empty() &&
@@ -257,11 +336,6 @@ static int plan_create_adaptive_impl(pcg_plan** out,
     int rc = plan_create_impl(out, N, L, frozen, n_frozen, systematic, crc_kind, device, fixed);
     if (rc != 0)
         return rc;
-    if (!fixed && (*out)->host.scl_kind != 0) {
-        pcg_plan_destroy(*out);
-        *out = nullptr;
-        return fail(PCG_E_UNSUPPORTED, "adaptive decoding needs the lane-serial SCL kernel");
-    }
     pcg_plan* fast = nullptr;
     // the Fast-SSC stage rejects what its constructor rejects (invalid_argument)
     rc = plan_create_impl(&fast, N, 1, frozen, n_frozen, systematic, crc_kind, device, fixed);
@@ -299,6 +373,21 @@ int pcg_plan_create_adaptive_char(pcg_plan** out,
     return plan_create_adaptive_impl(out, N, L, frozen, n_frozen, systematic, crc_kind, device, 1);
 }
 
+int pcg_plan_set_initial_metric(pcg_plan* p, float metric0)
+{
+    if (!p)
+        return fail(PCG_E_ARG, "null plan");
+    p->metric0 = metric0;
+    return PCG_OK;
+}
+
+const char* pcg_plan_kernel_name(const pcg_plan* p)
+{
+    if (!p)
+        return "";
+    return p->kernel;
+}
+
 int pcg_plan_describe(const pcg_plan* p, pcg_plan_desc* d)
 {
     if (!p || !d)
@@ -324,7 +413,8 @@ static int decode_impl(pcg_plan* p,
                        void* stream,
                        const uint32_t* fmap,
                        const uint32_t* fcount,
-                       const int8_t* llr8 = nullptr);
+                       const int8_t* llr8 = nullptr,
+                       float* soft = nullptr);
 
 static int decode_adaptive(pcg_plan* p, const float* llr, uint64_t F, uint8_t* info, uint8_t* ok, float* metrics,
                            void* stream, const int8_t* llr8 = nullptr)
@@ -387,7 +477,8 @@ static int decode_impl(pcg_plan* p,
                        void* stream,
                        const uint32_t* fmap,
                        const uint32_t* fcount,
-                       const int8_t* llr8)
+                       const int8_t* llr8,
+                       float* soft)
 {
     const auto& h = p->host;
     pcg::KernelArgs a{};
@@ -416,74 +507,49 @@ static int decode_impl(pcg_plan* p,
     a.fmap = fmap;
     a.fcount = fcount;
     a.llr8 = llr8;
-    if (getenv("PCG_OPPROF")) {
+    a.metric0 = p->metric0;
+    if (p->dev_opprof) {
         if (!g_prof && hipMalloc(&g_prof, 128 * sizeof(unsigned long long)) == hipSuccess)
             (void)hipMemset(g_prof, 0, 128 * sizeof(unsigned long long));
         a.prof = g_prof;
     }
-    if (const char* fl = getenv("PCG_FLAGS"))
-        a.flags = (uint32_t)strtoul(fl, nullptr, 0);
+    a.flags = p->dev_flags;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const bool i8 = llr8 != nullptr;
     int rc;
-    if (h.fixed && h.L == 1 && h.sc_kind == 0) {
-        const uint64_t need = pcg::sccs_units(F, p->wave_lds_floats, llr8 != nullptr);
-        if (p->scratch_floats > 0 && need > p->scratch_frames) {
-            (void)hipFree(p->d_scratch);
-            p->d_scratch = nullptr;
-            p->scratch_frames = 0;
-            hipError_t e = hipMalloc(&p->d_scratch, need * p->scratch_floats * sizeof(uint32_t));
-            if (e != hipSuccess)
-                return hip_fail(e, "hipMalloc(scratch)");
-            p->scratch_frames = need;
-        }
+    if (soft) { // soft codeword: the one-codeword-per-wave Fast-SSC kernel (float plans, L = 1)
+        a.soft = soft;
+        a.wave_lds_floats = pcg::sc_wave_lds_floats(h.N);
+        rc = pcg::launch_sc(a, s);
+    } else if (h.fixed && h.L == 1 && h.sc_kind == 0) {
+        a.units = (uint32_t)pcg::wave_units(F, 64, i8 ? p->wave_cap_i8 : p->wave_cap);
+        if ((rc = grow_scratch(p, a.units, sizeof(uint32_t), s)) != 0)
+            return rc;
         a.scratch = p->d_scratch;
         rc = pcg::launch_sccs(a, s);
     } else if (h.fixed && h.L == 1) {
         rc = pcg::launch_sc_char(a, s);
     } else if (h.fixed) {
-        const uint64_t need = pcg::sclc_units(F, h.L, p->wave_lds_floats, llr8 != nullptr);
-        if (p->scratch_floats > 0 && need > p->scratch_frames) {
-            (void)hipFree(p->d_scratch);
-            p->d_scratch = nullptr;
-            p->scratch_frames = 0;
-            hipError_t e = hipMalloc(&p->d_scratch, need * p->scratch_floats * sizeof(uint32_t));
-            if (e != hipSuccess)
-                return hip_fail(e, "hipMalloc(scratch)");
-            p->scratch_frames = need;
-        }
+        a.units = (uint32_t)pcg::wave_units(F, 64 / list_pow2(h.L), i8 ? p->wave_cap_i8 : p->wave_cap);
+        if ((rc = grow_scratch(p, a.units, sizeof(uint32_t), s)) != 0)
+            return rc;
         a.scratch = p->d_scratch;
         rc = pcg::launch_scl_char(a, s);
     } else if (h.L == 1 && h.sc_kind == 0) {
-        const uint64_t need = pcg::scs_units(F, p->wave_lds_floats);
-        if (p->scratch_floats > 0 && need > p->scratch_frames) {
-            (void)hipFree(p->d_scratch);
-            p->d_scratch = nullptr;
-            p->scratch_frames = 0;
-            hipError_t e = hipMalloc(&p->d_scratch, need * p->scratch_floats * sizeof(float));
-            if (e != hipSuccess)
-                return hip_fail(e, "hipMalloc(scratch)");
-            p->scratch_frames = need;
-        }
+        a.units = (uint32_t)pcg::wave_units(F, 64, p->wave_cap);
+        if ((rc = grow_scratch(p, a.units, sizeof(float), s)) != 0)
+            return rc;
         a.scratch = p->d_scratch;
         rc = pcg::launch_scs(a, s);
     } else if (h.L == 1) {
         rc = pcg::launch_sc(a, s);
     } else {
-        if (p->scratch_floats > 0) {
-            const uint64_t need = h.scl_kind == 0 ? pcg::sclls_units(F, h.L, p->wave_lds_floats)
-                                                  : pcg::scl_scratch_frames(F);
-            if (need > p->scratch_frames) {
-                (void)hipFree(p->d_scratch);
-                p->d_scratch = nullptr;
-                p->scratch_frames = 0;
-                hipError_t e = hipMalloc(&p->d_scratch, need * p->scratch_floats * sizeof(float));
-                if (e != hipSuccess)
-                    return hip_fail(e, "hipMalloc(scratch)");
-                p->scratch_frames = need;
-            }
-            a.scratch = p->d_scratch;
-        }
-        rc = h.scl_kind == 0 ? pcg::launch_sclls(a, s) : pcg::launch_scl(a, s);
+        a.units = (uint32_t)pcg::wave_units(F, 64 / list_pow2(h.L), p->wave_cap);
+        if ((rc = grow_scratch(p, a.units, sizeof(float), s)) != 0)
+            return rc;
+        a.scratch = p->d_scratch;
+        a.queue = p->d_queue;
+        rc = pcg::launch_sclls(a, s);
     }
     if (rc != 0)
         return fail(rc, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
@@ -620,6 +686,78 @@ int pcg_decode_f32_host(pcg_plan* p, const float* llr, uint64_t F, uint8_t* info
             return hip_fail(e, "hipMemcpy(D2H metrics)");
     }
     return PCG_OK;
+}
+
+static int soft_supported(const pcg_plan* p)
+{
+    if (!p)
+        return fail(PCG_E_ARG, "null plan");
+    if (p->host.L != 1 || p->host.fixed || p->fast)
+        return fail(PCG_E_UNSUPPORTED, "soft codewords: Fast-SSC float plans only (FastSscAvxFloat)");
+    if (pcg::sc_soft_lds_bytes(p->host.N) == 0)
+        return fail(PCG_E_UNSUPPORTED, "soft codewords: block length too large for one wave's LDS");
+    return PCG_OK;
+}
+
+int pcg_decode_f32_soft(pcg_plan* p,
+                        const float* llr,
+                        uint64_t F,
+                        uint8_t* info,
+                        uint8_t* ok,
+                        float* soft,
+                        void* stream)
+{
+    int rc = soft_supported(p);
+    if (rc != 0)
+        return rc;
+    if (F == 0)
+        return PCG_OK;
+    if (!llr || !info || !soft)
+        return fail(PCG_E_ARG, "null llr/info/soft buffer");
+    if (p->device < 0)
+        return fail(PCG_E_NODEVICE, "host-only plan (created with device < 0)");
+    if (F > 0xFFFFFFFFull)
+        return fail(PCG_E_ARG, "at most 2^32 - 1 frames per call");
+    DeviceGuard g(p->device);
+    return decode_impl(p, llr, F, info, ok, nullptr, stream, nullptr, nullptr, nullptr, soft);
+}
+
+int pcg_decode_f32_soft_host(pcg_plan* p, const float* llr, uint64_t F, uint8_t* info, uint8_t* ok, float* soft)
+{
+    int rc = soft_supported(p);
+    if (rc != 0)
+        return rc;
+    if (F == 0)
+        return PCG_OK;
+    if (!llr || !info || !soft)
+        return fail(PCG_E_ARG, "null llr/info/soft buffer");
+    if (p->device < 0)
+        return fail(PCG_E_NODEVICE, "host-only plan (created with device < 0)");
+    DeviceGuard g(p->device);
+    const uint64_t N = p->host.N, kb = (p->host.K + 7) / 8;
+    float* d_llr = nullptr;
+    float* d_soft = nullptr;
+    uint8_t* d_info = nullptr;
+    uint8_t* d_ok = nullptr;
+    hipError_t e;
+    if ((e = hipMalloc(&d_llr, F * N * sizeof(float))) != hipSuccess ||
+        (e = hipMalloc(&d_soft, F * N * sizeof(float))) != hipSuccess ||
+        (e = hipMalloc(&d_info, F * std::max<uint64_t>(kb, 1))) != hipSuccess ||
+        (e = hipMalloc(&d_ok, F)) != hipSuccess) {
+        rc = hip_fail(e, "hipMalloc(soft staging)");
+    } else if ((e = hipMemcpy(d_llr, llr, F * N * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess) {
+        rc = hip_fail(e, "hipMemcpy(H2D)");
+    } else if ((rc = pcg_decode_f32_soft(p, d_llr, F, d_info, d_ok, d_soft, nullptr)) == 0) {
+        if ((e = hipMemcpy(info, d_info, F * kb, hipMemcpyDeviceToHost)) != hipSuccess ||
+            (e = hipMemcpy(soft, d_soft, F * N * sizeof(float), hipMemcpyDeviceToHost)) != hipSuccess ||
+            (ok && (e = hipMemcpy(ok, d_ok, F, hipMemcpyDeviceToHost)) != hipSuccess))
+            rc = hip_fail(e, "hipMemcpy(D2H)");
+    }
+    (void)hipFree(d_llr);
+    (void)hipFree(d_soft);
+    (void)hipFree(d_info);
+    (void)hipFree(d_ok);
+    return rc;
 }
 
 int pcg_decode_punctured_f32(pcg_plan* p,

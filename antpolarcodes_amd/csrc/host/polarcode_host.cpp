@@ -347,9 +347,14 @@ void Decoder::setSignal(const float* pLlr)
     mSignalI8 = false;
 }
 
-void Decoder::setSignal(const char* pLlr) // FloatContainer::insertLlr(const char*), bitcontainer.cpp:202-207
+void Decoder::setSignal(const char* pLlr)
 {
-    for (size_t i = 0; i < mBlockLength; ++i)
+    if (mCharContainer) { // CharContainer::insertLlr(const char*): a copy
+        mLlr8.assign(pLlr, pLlr + mBlockLength);
+        mSignalI8 = true;
+        return;
+    }
+    for (size_t i = 0; i < mBlockLength; ++i) // FloatContainer::insertLlr(const char*), bitcontainer.cpp:202-207
         mLlr[i] = static_cast<float>(pLlr[i]);
     mSignalI8 = false;
 }
@@ -357,6 +362,57 @@ void Decoder::setSignal(const char* pLlr) // FloatContainer::insertLlr(const cha
 void Decoder::getDecodedInformationBits(void* pData)
 {
     std::memcpy(pData, mOutputContainer.data(), (mBlockLength - mFrozenBits.size() + 7) / 8);
+}
+
+void Decoder::getSoftCodeword(void* pData)
+{
+    if (mSoftCodeword.size() != mBlockLength)
+        throw std::logic_error("no soft codeword: decode() a frame with a Fast-SSC float decoder first");
+    std::memcpy(pData, mSoftCodeword.data(), mBlockLength * sizeof(float));
+}
+
+void Decoder::getSoftInformation(void* pData)
+{
+    if (mSoftCodeword.size() != mBlockLength)
+        throw std::logic_error("no soft codeword: decode() a frame with a Fast-SSC float decoder first");
+    std::vector<uint8_t> isf(mBlockLength, 0);
+    for (unsigned f : mFrozenBits)
+        isf[f] = 1;
+    float* out = static_cast<float*>(pData);
+    for (size_t i = 0; i < mBlockLength; ++i) // the LUT order: info positions ascending
+        if (!isf[i])
+            *out++ = mSoftCodeword[i];
+}
+
+bool Decoder::decodeBatch(const float* llr, size_t F, uint8_t* info, uint8_t* ok, float*)
+{
+    const size_t kb = (infoLength() + 7) / 8;
+    bool all = true;
+    for (size_t f = 0; f < F; ++f) {
+        const bool r = decode_vector(llr + f * mBlockLength, info + f * kb);
+        if (ok)
+            ok[f] = r ? 1 : 0;
+        all = all && r;
+    }
+    return all;
+}
+
+void Decoder::decodeBatchDevice(const float*, size_t, uint8_t*, uint8_t*, float*, void*)
+{
+    throw std::logic_error("decodeBatchDevice needs a GPU decoder");
+}
+
+bool Decoder::decodeBatchI8(const int8_t* llr, size_t F, uint8_t* info, uint8_t* ok, float*)
+{
+    const size_t kb = (infoLength() + 7) / 8;
+    bool all = true;
+    for (size_t f = 0; f < F; ++f) {
+        const bool r = decode_vector(reinterpret_cast<const char*>(llr) + f * mBlockLength, info + f * kb);
+        if (ok)
+            ok[f] = r ? 1 : 0;
+        all = all && r;
+    }
+    return all;
 }
 
 bool Decoder::decode_vector(const float* pLlr, void* pData)
@@ -456,21 +512,39 @@ void GpuDecoder::ensurePlan()
     mPlanSys = mSystematic;
 }
 
-void GpuDecoder::setSignal(const char* pLlr)
-{
-    if (!mFixed)
-        return Decoder::setSignal(pLlr);
-    mLlr8.assign(pLlr, pLlr + mBlockLength); // CharContainer::insertLlr(const char*): a copy
-    mSignalI8 = true;
-}
-
 bool GpuDecoder::decode()
 {
+    // one frame of one reused decoder instance: Fast-SSC float decoders also return the
+    // soft codeword (getSoftCodeword); list decoders start from the carried path-0 metric
+    // and keep the new one (the reference's PathList never resets mMetric, Q8)
+    ensurePlan();
     uint8_t ok = 0;
-    if (mSignalI8)
-        decodeBatchI8(mLlr8.data(), 1, mOutputContainer.data(), &ok, nullptr);
-    else
-        decodeBatch(mLlr.data(), 1, mOutputContainer.data(), &ok, nullptr);
+    int rc;
+    if (mListSize <= 1 && !mFixed && !mAdaptive && !mSignalI8) {
+        mSoftCodeword.resize(mBlockLength);
+        rc = pcg_decode_f32_soft_host(mPlan, mLlr.data(), 1, mOutputContainer.data(), &ok, mSoftCodeword.data());
+        if (rc != 0) {
+            mSoftCodeword.clear();
+            throw_pcg(rc);
+        }
+    } else {
+        // (the adaptive decoders' list stage runs only for failed frames: no carry there)
+        const bool carry = mListSize > 1 && !mAdaptive;
+        std::vector<float> met(mListSize > 1 ? mListSize : 1, 0.0f);
+        float* mp = carry ? met.data() : nullptr;
+        if (carry && (rc = pcg_plan_set_initial_metric(mPlan, mCarry)) != 0)
+            throw_pcg(rc);
+        if (mSignalI8)
+            rc = pcg_decode_i8_host(mPlan, mLlr8.data(), 1, mOutputContainer.data(), &ok, mp);
+        else
+            rc = pcg_decode_f32_host(mPlan, mLlr.data(), 1, mOutputContainer.data(), &ok, mp);
+        if (carry)
+            (void)pcg_plan_set_initial_metric(mPlan, 0.0f); // batches keep fresh-decoder semantics
+        if (rc != 0)
+            throw_pcg(rc);
+        if (carry)
+            mCarry = met[0];
+    }
     mLastOk = ok != 0;
     return mLastOk;
 }
@@ -541,6 +615,7 @@ GpuFastSscChar::GpuFastSscChar(size_t blockLength, const std::vector<unsigned>& 
     : GpuDecoder(blockLength, 1, {}, device)
 {
     mFixed = true;
+    mCharContainer = true;
     initialize(blockLength, frozenBits);
 }
 
@@ -548,6 +623,7 @@ GpuSclChar::GpuSclChar(size_t blockLength, size_t listSize, const std::vector<un
     : GpuDecoder(blockLength, listSize, {}, device)
 {
     mFixed = true;
+    mCharContainer = true;
     initialize(blockLength, frozenBits);
 }
 
@@ -557,6 +633,7 @@ GpuAdaptiveChar::GpuAdaptiveChar(size_t blockLength, size_t listSize, const std:
 {
     mAdaptive = true;
     mFixed = true;
+    mCharContainer = true;
     initialize(blockLength, frozenBits);
 }
 

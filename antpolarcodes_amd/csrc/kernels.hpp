@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace pcg {
 
@@ -39,7 +40,26 @@ struct KernelArgs {
     // counts differ) and the last wave to finish zeroes both for the next launch.
     // null -> static grid-stride assignment.
     uint32_t* queue;
+    // grid size (persistent waves) chosen by the caller: min(groups, the plan's wave cap)
+    uint32_t units;
+    // SCL: initial path-0 metric of every frame (0 = a freshly constructed decoder; the
+    // previous frame's final path-0 metric reproduces the reference's carry across frames of
+    // one decoder instance)
+    float metric0;
+    // Fast-SSC (sc_kernel.hip): F x N soft codeword output (Decoder::getSoftCodeword) or null
+    float* soft;
 };
+
+// PCG_*_WPC developer overrides of the waves per CU: ignored unless a positive number
+inline uint64_t env_wpc(const char* name, uint64_t dflt)
+{
+    if (const char* e = getenv(name)) {
+        const long v = strtol(e, nullptr, 10);
+        if (v > 0 && v <= 64)
+            return (uint64_t)v;
+    }
+    return dflt;
+}
 
 // Dynamic group assignment for the persistent lane-serial kernels (KernelArgs::queue;
 // one-wave workgroups). Every lane gets the same ticket; a wave stops at its first ticket
@@ -66,35 +86,36 @@ __device__ inline void queue_retire(uint32_t* q)
 // LDS floats one SC codeword needs: alpha (N floats, index 0 unused) + packed bits.
 inline uint32_t sc_wave_lds_floats(uint32_t N) { return N + (N >= 64 ? N / 32 : 2) + 2; }
 
-int launch_sc(const KernelArgs& a, hipStream_t stream);
+int launch_sc(const KernelArgs& a, hipStream_t stream); // one codeword per wave; a.soft: + soft codeword
+uint32_t sc_soft_lds_bytes(uint32_t N);                  // 0: N too large for the soft-output decode
 int launch_sc_char(const KernelArgs& a, hipStream_t stream);   // FastSscFipChar (sc_char_kernel.hip)
 int launch_scl_char(const KernelArgs& a, hipStream_t stream);  // SclFipChar (scl_char_kernel.hip)
-int launch_scl(const KernelArgs& a, hipStream_t stream);
 
 } // namespace pcg
 
 namespace pcg {
-// SCL LDS / scratch layout for (N, L): returns 0 or PCG_E_UNSUPPORTED.
-int scl_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* lds_stage_limit,
-               uint64_t* scratch_floats);
-// codewords that need scratch at once for a launch of F frames
-uint64_t scl_scratch_frames(uint64_t F);
-// lane-serial SCL kernel (sclls_kernel.hip): per-wave LDS / scratch layout, the
-// number of scratch units (waves) a launch of F frames uses, and the launch
+// Persistent lane-serial kernels: per-wave LDS / global scratch layout, the wave cap of a
+// launch on the current device (CUs x resident waves per CU from hipOccupancy; evaluated
+// once per plan), and the launch (grid = KernelArgs::units)
+inline uint64_t wave_units(uint64_t F, uint32_t frames_per_wave, uint64_t cap)
+{
+    const uint64_t need = (F + frames_per_wave - 1) / frames_per_wave;
+    return need < cap ? need : cap;
+}
+// lane-serial SCL kernel (sclls_kernel.hip), 64 / L' codewords per wave
 int sclls_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* lds_stage_limit,
                  uint64_t* scratch_floats, uint32_t* virt);
-uint64_t sclls_units(uint64_t F, uint32_t L, uint32_t wave_lds_floats);
+uint64_t sclls_wave_cap(uint32_t L, uint32_t wave_lds_floats);
 int launch_sclls(const KernelArgs& a, hipStream_t stream);
-// 8-bit SCL (scl_char_kernel.hip): LDS dwords per wave, LDS stage limit, global scratch
-// dwords per wave; persistent waves for a launch of F frames
+// 8-bit SCL (scl_char_kernel.hip): LDS dwords per wave, LDS stage limit, global scratch dwords
 int sclc_layout(uint32_t N, uint32_t L, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratch_dwords);
-uint64_t sclc_units(uint64_t F, uint32_t L, uint32_t lds_dwords, bool i8);
-// lane-serial Fast-SSC (scs_kernel.hip): layout, persistent waves, launch
+uint64_t sclc_wave_cap(uint32_t L, uint32_t lds_dwords, bool i8);
+// lane-serial Fast-SSC (scs_kernel.hip), 64 codewords per wave
 int scs_layout(uint32_t N, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratch_dwords);
-uint64_t scs_units(uint64_t F, uint32_t lds_dwords);
+uint64_t scs_wave_cap(uint32_t lds_dwords);
 int launch_scs(const KernelArgs& a, hipStream_t stream);
-// lane-serial 8-bit Fast-SSC (sccs_kernel.hip)
+// lane-serial 8-bit Fast-SSC (sccs_kernel.hip), 64 codewords per wave
 int sccs_layout(uint32_t N, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratch_dwords);
-uint64_t sccs_units(uint64_t F, uint32_t lds_dwords, bool i8);
+uint64_t sccs_wave_cap(uint32_t lds_dwords, bool i8);
 int launch_sccs(const KernelArgs& a, hipStream_t stream);
 } // namespace pcg

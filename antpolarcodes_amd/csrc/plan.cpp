@@ -268,8 +268,13 @@ int build_plan(PlanHost& p,
                int fixed)
 {
     p = PlanHost();
-    if (N < 8 || N > 32768 || (N & (N - 1))) {
-        *err = "block length must be a power of two in [8, 32768]";
+    // Fast-SSC float plans run codes down to N = 2 (the reference's own Repetition /
+    // SPC KATs start there, decodingtest.cpp:185-195); the lane-serial list and 8-bit
+    // kernels need N >= 8
+    const uint32_t nmin = (L == 1 && !fixed) ? 2u : 8u;
+    if (N < nmin || N > 32768 || (N & (N - 1))) {
+        *err = nmin == 2 ? "block length must be a power of two in [2, 32768]"
+                         : "block length must be a power of two in [8, 32768]";
         return -1;
     }
     if (L < 1 || L > 32) {
@@ -298,18 +303,10 @@ int build_plan(PlanHost& p,
     p.crc_kind = crc_kind;
     p.frozen.assign(frozen, frozen + nf);
     p.fixed = fixed ? 1 : 0;
-    // SCL kernel choice (dev switch PCG_SCL_KERNEL=wave selects the cooperative
-    // one-codeword-per-wave kernel); the lane-serial kernel always runs size-8
-    // subtrees in registers, the cooperative one only for L <= 8 (<= 64 candidates)
-    {
-        const char* k = getenv("PCG_SCL_KERNEL");
-        p.scl_kind = (k && std::string(k) == "wave") ? 1 : 0;
-    }
     {
         const char* k = getenv("PCG_SC_KERNEL"); // dev switch: "wave" = sc_kernel.hip
         p.sc_kind = (k && std::string(k) == "wave") ? 1 : 0;
     }
-    p.scl_st8 = p.scl_kind == 0 || (L <= 8 && getenv("PCG_SCL_NO_ST8") == nullptr);
     try {
         if (p.fixed && L == 1)
             sc_char_emit(p, p.frozen, N, 0);

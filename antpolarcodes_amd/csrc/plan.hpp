@@ -91,7 +91,6 @@ struct PlanHost {
     uint32_t node_count = 0;
     std::vector<int> node_types;    // pre-order census (op code of each node; 0 = internal)
     bool scl_st8 = true;            // emit lane-serial size-8 subtrees for SCL
-    int scl_kind = 0;               // SCL kernel: 0 lane-serial (sclls_kernel.hip), 1 one codeword per wave
     int fixed = 0;                  // 1: the reference's 8-bit decoders (FastSscFipChar / SclFipChar)
     int sc_kind = 0;                // Fast-SSC kernel: 0 lane-serial (scs_kernel.hip), 1 one codeword per wave
 };

@@ -158,6 +158,23 @@ PYBIND11_MODULE(_pypolar, m)
                  std::memcpy(res.request().ptr, tmp.data(), s.dec->infoLength() / 8);
                  return res;
              })
+        .def("getSoftCodeword", // Decoder::getSoftCodeword after decode_vector (Fast-SSC float)
+             [](PyDecoder& s) {
+                 py::array_t<float> out(s.dec->blockLength());
+                 s.dec->getSoftCodeword(out.mutable_data());
+                 return out;
+             })
+        .def("getSoftInformation",
+             [](PyDecoder& s) {
+                 py::array_t<float> out(s.dec->infoLength());
+                 s.dec->getSoftInformation(out.mutable_data());
+                 return out;
+             })
+        .def("carriedMetric", // SCL: path 0's metric the next decode_vector starts from (Q8)
+             [](PyDecoder& s) {
+                 auto* g = dynamic_cast<Decoding::GpuDecoder*>(s.dec.get());
+                 return g ? g->carriedMetric() : 0.0f;
+             })
         .def(
             "decode_batch",
             [](PyDecoder& s, const f32array& a, bool return_ok, bool return_metrics) {

@@ -495,8 +495,11 @@ int sccs_layout(uint32_t N, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratc
     for (uint32_t s = 0; s <= top - 1; ++s)
         if (cs_layout(N, s).lds * 4u <= budget)
             best = s;
-    if (const char* e = getenv("PCG_SCCS_SL"))
-        best = (uint32_t)atoi(e);
+    if (const char* e = getenv("PCG_SCCS_SL")) { // dev override, ignored when out of range
+        const uint32_t v = (uint32_t)atoi(e);
+        if (v <= top - 1)
+            best = v;
+    }
     const CsLayout y = cs_layout(N, best);
     if (y.lds * 4u > 160u * 1024u)
         return -4;
@@ -506,7 +509,7 @@ int sccs_layout(uint32_t N, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratc
     return 0;
 }
 
-uint64_t sccs_units(uint64_t F, uint32_t lds_dwords, bool i8)
+uint64_t sccs_wave_cap(uint32_t lds_dwords, bool i8)
 {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess)
@@ -515,20 +518,17 @@ uint64_t sccs_units(uint64_t F, uint32_t lds_dwords, bool i8)
     uint64_t wpc = res > 0 ? (uint64_t)res : 1;
     if (wpc > 16)
         wpc = 16;
-    if (const char* e = getenv("PCG_SCCS_WPC"))
-        wpc = (uint64_t)atoi(e);
+    wpc = env_wpc("PCG_SCCS_WPC", wpc);
     if (getenv("PCG_DEBUG_OCC"))
         fprintf(stderr, "[pcg] sccs: lds %u B, resident %d waves/CU, using %llu\n", lds_dwords * 4u, res,
                 (unsigned long long)wpc);
-    const uint64_t need = (F + 63) / 64;
-    const uint64_t cap = (uint64_t)cus * wpc;
-    return need < cap ? need : cap;
+    return (uint64_t)cus * wpc;
 }
 
 int launch_sccs(const KernelArgs& a, hipStream_t stream)
 {
     const bool i8 = a.llr8 != nullptr;
-    const uint64_t grid = sccs_units(a.F, a.wave_lds_floats, i8);
+    const uint64_t grid = a.units;
     if (grid == 0)
         return 0;
     const size_t lds = (size_t)a.wave_lds_floats * 4u;

@@ -9,7 +9,8 @@
 //
 // Path state of lane l = g*LP + p:
 //   * metric (int32; the reference's `long` metrics are exact integers bounded by
-//     128 N per frame, and every frame starts from 0 -- see DESIGN.md Q8);
+//     128 N per frame; a frame starts from 0, or from the carried metric of a reused
+//     decoder instance -- see DESIGN.md Q8);
 //   * LLR bytes of stages s < top-1 in 16-byte units, unit c of lane l's column at
 //     [(c * 64) + l] of the stage region (LDS for s < Sl, a per-wave global slab for
 //     Sl <= s < top-1), so a wave-wide unit access is one contiguous 1 KiB, addressed through a 5-bit-per-stage slot table (the lane that
@@ -549,7 +550,7 @@ __global__ void __launch_bounds__(64) scl_char_kernel(KernelArgs a, uint32_t Sl)
         else
             w.chan = a.llr + frame * a.N;
         w.ptr = 0;
-        w.m = 0;
+        w.m = (int)a.metric0; // 0, or the carried metric of a reused decoder (Q8)
         w.right = false;
         uint32_t P = 1;
         SC_T0(tg0);
@@ -702,8 +703,11 @@ int sclc_layout(uint32_t N, uint32_t L, uint32_t* lds_dwords, uint32_t* Sl, uint
     for (uint32_t s = 0; s <= top - 1; ++s)
         if (make_layout(N, s).lds * 4u <= budget)
             best = s;
-    if (const char* e = getenv("PCG_SCLC_SL"))
-        best = (uint32_t)atoi(e);
+    if (const char* e = getenv("PCG_SCLC_SL")) { // dev override, ignored when out of range
+        const uint32_t v = (uint32_t)atoi(e);
+        if (v <= top - 1)
+            best = v;
+    }
     const Layout y = make_layout(N, best);
     if (y.lds * 4u > 160u * 1024u)
         return -4;
@@ -713,7 +717,7 @@ int sclc_layout(uint32_t N, uint32_t L, uint32_t* lds_dwords, uint32_t* Sl, uint
     return 0;
 }
 
-uint64_t sclc_units(uint64_t F, uint32_t L, uint32_t lds_dwords, bool i8)
+uint64_t sclc_wave_cap(uint32_t L, uint32_t lds_dwords, bool i8)
 {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess)
@@ -730,21 +734,17 @@ uint64_t sclc_units(uint64_t F, uint32_t L, uint32_t lds_dwords, bool i8)
     uint64_t wpc = res > 0 ? (uint64_t)res : 1;
     if (wpc > 16)
         wpc = 16;
-    if (const char* e = getenv("PCG_SCLC_WPC"))
-        wpc = (uint64_t)atoi(e);
+    wpc = env_wpc("PCG_SCLC_WPC", wpc);
     if (getenv("PCG_DEBUG_OCC"))
         fprintf(stderr, "[pcg] sclc: lds %u B, resident %d waves/CU, using %llu\n", lds, res,
                 (unsigned long long)wpc);
-    const uint64_t G = 64 / lp_of(L);
-    const uint64_t need = (F + G - 1) / G;
-    const uint64_t cap = (uint64_t)cus * wpc;
-    return need < cap ? need : cap;
+    return (uint64_t)cus * wpc;
 }
 
 int launch_scl_char(const KernelArgs& a, hipStream_t stream)
 {
     const bool i8 = a.llr8 != nullptr;
-    const uint64_t grid = sclc_units(a.F, a.L, a.wave_lds_floats, i8);
+    const uint64_t grid = a.units;
     if (grid == 0)
         return 0;
     const size_t lds = (size_t)a.wave_lds_floats * 4u;

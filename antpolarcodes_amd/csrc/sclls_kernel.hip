@@ -1164,13 +1164,19 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
     const uint32_t W = a.N >= 32 ? a.N / 32 : 1u;
 
     const uint64_t Fn = a.fcount ? (uint64_t)*a.fcount : a.F;
-    for (uint64_t fb = (uint64_t)blockIdx.x * G; fb < Fn; fb += (uint64_t)gridDim.x * G) {
+    // codeword groups: from the plan's work queue (dynamic balance across SIMDs whose
+    // resident wave counts differ), else a static grid stride
+    const uint64_t stride = (uint64_t)gridDim.x * G;
+    for (uint64_t fb = a.queue ? queue_next(a.queue) * G : (uint64_t)blockIdx.x * G; fb < Fn;
+         fb = a.queue ? queue_next(a.queue) * G : fb + stride) {
         const uint64_t slot = fb + c.lane / LP;
         const bool fvalid = slot < Fn;
         const uint64_t fs = fvalid ? slot : Fn - 1;
         const uint64_t frame = a.fmap ? (uint64_t)a.fmap[fs] : fs;
         c.y = a.llr + frame * a.N;
-        c.m = 0.0f; // a freshly constructed decoder
+        // path 0 starts at 0 (a freshly constructed decoder) or, for a reused decoder
+        // instance, at the previous frame's final path-0 metric
+        c.m = a.metric0;
         c.ptr = 0;
         uint32_t P = 1;
 #ifdef PCG_LS_PROF
@@ -1272,6 +1278,8 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
         }
 #endif
     }
+    if (a.queue)
+        queue_retire(a.queue);
 #ifdef PCG_LS_PROF
     wsync();
     if (c.lane == 0 && a.prof)
@@ -1337,7 +1345,7 @@ static int ls_resident(uint32_t lds_bytes)
 
 // Waves (= scratch units) for a launch of F frames: one persistent wave per resident
 // slot (hipOccupancy: VGPR / LDS limits), capped at PCG_SCL_WPC waves per CU.
-uint64_t sclls_units(uint64_t F, uint32_t L, uint32_t wave_lds_floats)
+uint64_t sclls_wave_cap(uint32_t L, uint32_t wave_lds_floats)
 {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess)
@@ -1354,24 +1362,16 @@ uint64_t sclls_units(uint64_t F, uint32_t L, uint32_t wave_lds_floats)
     uint64_t wpc = res > 0 ? (uint64_t)res : 1;
     if (wpc > 8)
         wpc = 8;
-    // L = 32 (N = 4096: 5 resident waves/CU, SIMDs at 2-1-1-1): oversubscribe so the
-    // dispatcher balances groups across SIMDs (measured 3.27e5 -> 4.11e5 cw/s at 32/CU)
-    if (lp_of(L) == 32)
-        wpc = 32;
-    if (const char* e = getenv("PCG_SCL_WPC"))
-        wpc = (uint64_t)atoi(e);
+    wpc = env_wpc("PCG_SCL_WPC", wpc);
     if (getenv("PCG_DEBUG_OCC"))
         fprintf(stderr, "[pcg] sclls: lds %u B, resident %d waves/CU, using %llu\n", lds, res,
                 (unsigned long long)wpc);
-    const uint64_t G = 64 / lp_of(L);
-    const uint64_t need = (F + G - 1) / G;
-    const uint64_t cap = (uint64_t)cus * wpc;
-    return need < cap ? need : cap;
+    return (uint64_t)cus * wpc;
 }
 
 int launch_sclls(const KernelArgs& a, hipStream_t stream)
 {
-    const uint64_t grid = sclls_units(a.F, a.L, a.wave_lds_floats);
+    const uint64_t grid = a.units;
     if (grid == 0)
         return 0;
     size_t lds = (size_t)a.wave_lds_floats * sizeof(float);

@@ -640,8 +640,11 @@ int scs_layout(uint32_t N, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratch
     for (uint32_t s = 1; s <= top - 1; ++s)
         if (ss_layout(N, s).lds * 4u <= budget)
             best = s;
-    if (const char* e = getenv("PCG_SCS_SL"))
-        best = (uint32_t)atoi(e);
+    if (const char* e = getenv("PCG_SCS_SL")) { // dev override, ignored when out of range
+        const uint32_t v = (uint32_t)atoi(e);
+        if (v >= 1 && v <= top - 1)
+            best = v;
+    }
     const SsLayout y = ss_layout(N, best);
     if (y.lds * 4u > 160u * 1024u)
         return -4;
@@ -651,7 +654,7 @@ int scs_layout(uint32_t N, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratch
     return 0;
 }
 
-uint64_t scs_units(uint64_t F, uint32_t lds_dwords)
+uint64_t scs_wave_cap(uint32_t lds_dwords)
 {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess)
@@ -660,19 +663,16 @@ uint64_t scs_units(uint64_t F, uint32_t lds_dwords)
     uint64_t wpc = res > 0 ? (uint64_t)res : 1;
     if (wpc > 16)
         wpc = 16;
-    if (const char* e = getenv("PCG_SCS_WPC"))
-        wpc = (uint64_t)atoi(e);
+    wpc = env_wpc("PCG_SCS_WPC", wpc);
     if (getenv("PCG_DEBUG_OCC"))
         fprintf(stderr, "[pcg] scs: lds %u B, resident %d waves/CU, using %llu\n", lds_dwords * 4u, res,
                 (unsigned long long)wpc);
-    const uint64_t need = (F + 63) / 64;
-    const uint64_t cap = (uint64_t)cus * wpc;
-    return need < cap ? need : cap;
+    return (uint64_t)cus * wpc;
 }
 
 int launch_scs(const KernelArgs& a, hipStream_t stream)
 {
-    const uint64_t grid = scs_units(a.F, a.wave_lds_floats);
+    const uint64_t grid = a.units;
     if (grid == 0)
         return 0;
     hipLaunchKernelGGL(scs_kernel, dim3((uint32_t)grid), dim3(64), (size_t)a.wave_lds_floats * 4u, stream, a,

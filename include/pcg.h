@@ -18,6 +18,8 @@
  *   pcg_decode_f32    <- Decoder::decode_vector(const float*, void*) decoder.cpp:154-167,
  *                        batched: F frames per call, device-resident buffers
  *   pcg_decode_f32_host <- the same with host buffers (H2D + decode + D2H)
+ *   pcg_decode_f32_soft[_host] <- decode + Decoder::getSoftCodeword (decoder.cpp:147,
+ *                        FloatContainer::getSoftBits bitcontainer.cpp:294-297)
  *   pcg_plan_create_adaptive <- makeDecoder(..., 2) = AdaptiveFloat, decoder.cpp:75,
  *                        adaptive_float.cpp:14-45 (SC first, SCL for the failures)
  *   pcg_plan_create_char <- Decoding::create(..., "char") / makeDecoder(..., 0): the 8-bit
@@ -41,9 +43,20 @@
  *                        (src/simulation/simulator.cpp:850-937, bpsk.cpp:54-80,
  *                        awgn.cpp:38-43), counter-based and reproducible from a seed
  *
+ *   pcg_plan_set_initial_metric <- the SCL path-metric carry of a reused decoder
+ *                        instance (PathList::setFirstPath keeps mMetric[0],
+ *                        scl_avx_float.cpp:31, 99-109)
+ *
  * Error model: every function returns 0 on success or a negative PCG_E* code;
  * nothing throws across the ABI.  pcg_last_error() (thread-local) describes the
  * most recent failure on the calling thread.
+ *
+ * Threading: a plan is like the reference's stateful Decoder objects (one per
+ * worker thread, simulator.cpp:703-764): its scratch, work queue, staging and
+ * adaptive frame-map buffers are reused by every decode call, so all decode entry
+ * points on one plan must be issued from one host thread on one stream (calls on
+ * one stream are ordered; two streams would race on the plan's buffers).  Plans are
+ * independent of each other: one plan per stream / per GPU runs concurrently.
  */
 #ifndef PCG_H
 #define PCG_H
@@ -139,6 +152,28 @@ int pcg_decode_f32_host(pcg_plan* plan,
                         uint8_t* ok,
                         float* metrics);
 
+/* Fast-SSC float plans (L == 1): decode as pcg_decode_f32 and also write each frame's soft
+ * codeword -- the reference's root FloatContainer word for word (Decoder::getSoftCodeword,
+ * decoder.cpp:147; the leaf decoders' float outputs combined by the full 32-bit XOR of
+ * RateRNode, fastssc_avx_float.cpp:148-792).  soft: device F x N floats.  Runs the
+ * one-codeword-per-wave kernel (slower than pcg_decode_f32).  PCG_E_UNSUPPORTED for list,
+ * 8-bit and adaptive plans and for N whose state exceeds a CU's LDS (N > 16384). */
+int pcg_decode_f32_soft(pcg_plan* plan,
+                        const float* llr,
+                        uint64_t F,
+                        uint8_t* info,
+                        uint8_t* ok,
+                        float* soft,
+                        void* stream);
+
+/* Same with HOST pointers; synchronous. */
+int pcg_decode_f32_soft_host(pcg_plan* plan,
+                             const float* llr,
+                             uint64_t F,
+                             uint8_t* info,
+                             uint8_t* ok,
+                             float* soft);
+
 /* An 8-bit fixed-point plan: the reference's "char" decoders (FastSscFipChar for L == 1,
  * SclFipChar for L >= 2; L <= 32), classified and computed exactly as they are
  * (saturating int8 LLRs, integer path metrics).  Decode int8 frames with pcg_decode_i8, or
@@ -187,6 +222,17 @@ int pcg_decode_i8_host(pcg_plan* plan,
                        float* metrics);
 
 int pcg_plan_describe(const pcg_plan* plan, pcg_plan_desc* desc);
+
+/* Name of the kernel a decode on this plan launches (e.g. "sclls_kernel<8>",
+ * "scs_kernel"), as it appears in rocprofv3 kernel traces; "" for NULL. */
+const char* pcg_plan_kernel_name(const pcg_plan* plan);
+
+/* SCL plans: the metric path 0 starts every frame of later decode calls with.  0 (the
+ * default) is a freshly constructed reference decoder; passing the previous frame's final
+ * metrics[0] reproduces a reference decoder instance reused frame after frame (its
+ * PathList never resets mMetric, scl_avx_float.cpp:31, 99-109).  For the
+ * 8-bit plans the value is converted to the integer metric.  Ignored by Fast-SSC. */
+int pcg_plan_set_initial_metric(pcg_plan* plan, float metric0);
 
 void pcg_plan_destroy(pcg_plan* plan);
 

@@ -35,6 +35,8 @@ protected:
     bool mSignalI8 = false;                   ///< the pending frame is mLlr8
     std::vector<unsigned char> mOutputContainer;
     bool mLastOk = false;
+    bool mCharContainer = false;              ///< 8-bit decoder: setSignal(const char*) keeps the bytes
+    std::vector<float> mSoftCodeword;         ///< soft codeword of the last decode() (empty: none)
 
 public:
     Decoder();
@@ -63,22 +65,38 @@ public:
     }
     virtual size_t getListSize() { return 1; }
     virtual void setSignal(const float* pLlr);
-    /// 8-bit LLRs: float decoders convert them (FloatContainer::insertLlr(const char*),
-    /// bitcontainer.cpp:202-207); 8-bit decoders take them as they are.
-    virtual void setSignal(const char* pLlr);
+    /// 8-bit LLRs (non-virtual, as in the reference, decoder.h:170): float decoders convert
+    /// them (FloatContainer::insertLlr(const char*), bitcontainer.cpp:202-207); 8-bit
+    /// decoders take them as they are (CharContainer::insertLlr).
+    void setSignal(const char* pLlr);
     void getDecodedInformationBits(void* pData);
+    /// The last decode()'s soft codeword, N floats (FloatContainer::getSoftBits,
+    /// bitcontainer.cpp:294-297): the root bit container word for word.  Available from
+    /// the Fast-SSC float decoder; std::logic_error for decoders whose GPU kernels keep
+    /// hard decisions only (SCL, 8-bit, adaptive).
+    void getSoftCodeword(void* pData);
+    /// The soft codeword at the information positions, K floats
+    /// (FloatContainer::getSoftInformation, bitcontainer.cpp:331-339).
+    void getSoftInformation(void* pData);
+    /// Direct access to the decoder's input LLRs (N floats) and soft output (N floats,
+    /// empty before a soft-capable decode).  The reference returns its BitContainer
+    /// objects here (decoder.h:107-108); this build has no container classes.
+    float* inputContainer() { return mLlr.data(); }
+    float* outputContainer() { return mSoftCodeword.empty() ? nullptr : mSoftCodeword.data(); }
 
     /// Batched decode of F frames (host memory): llr F x N, info F x ceil(K/8),
-    /// ok F (nullable), metrics F x L (nullable, SCL only).  Returns true if every
-    /// frame passed the detector.
+    /// ok F (nullable), metrics F x L (nullable, list decoders only).  Returns true if
+    /// every frame passed the detector.  The default decodes frame by frame through
+    /// decode_vector (metrics left untouched); the GPU decoders run one batched launch.
     virtual bool decodeBatch(const float* llr, size_t F, uint8_t* info, uint8_t* ok = nullptr,
-                             float* metrics = nullptr) = 0;
+                             float* metrics = nullptr);
     /// Same with device pointers, asynchronous on `hipStream` (null = default stream).
+    /// The default raises std::logic_error (a CPU decoder has no device path).
     virtual void decodeBatchDevice(const float* llr, size_t F, uint8_t* info, uint8_t* ok = nullptr,
-                                   float* metrics = nullptr, void* hipStream = nullptr) = 0;
-    /// Batched decode of F frames of int8 LLRs (host memory).
+                                   float* metrics = nullptr, void* hipStream = nullptr);
+    /// Batched decode of F frames of int8 LLRs (host memory); default: decode_vector(const char*).
     virtual bool decodeBatchI8(const int8_t* llr, size_t F, uint8_t* info, uint8_t* ok = nullptr,
-                               float* metrics = nullptr) = 0;
+                               float* metrics = nullptr);
 };
 
 /// Shared GPU plumbing: owns one pcg_plan, rebuilt when code / detector / systematic
@@ -93,6 +111,9 @@ protected:
     bool mPlanSys = true;
     bool mAdaptive = false; ///< pcg_plan_create_adaptive (Fast-SSC first, SCL for failures)
     bool mFixed = false;    ///< pcg_plan_create_char (the reference's 8-bit decoders)
+    /// SCL: path 0's final metric of the last decode(), the next decode()'s start metric --
+    /// one reference decoder instance reused frame after frame
+    float mCarry = 0.0f;
     void ensurePlan();
     void releasePlan();
 
@@ -113,9 +134,9 @@ public:
     /// int8 frames in device memory (8-bit decoders only), asynchronous on `hipStream`.
     void decodeBatchDeviceI8(const int8_t* llr, size_t F, uint8_t* info, uint8_t* ok = nullptr,
                              float* metrics = nullptr, void* hipStream = nullptr);
-    void setSignal(const char* pLlr) override;
-    using Decoder::setSignal;
     bool isFixedPoint() const { return mFixed; }
+    /// SCL: the start metric the next decode() carries (0 after construction).
+    float carriedMetric() const { return mCarry; }
     int device() const { return mDevice; }
 };
 

@@ -75,3 +75,37 @@ def test_scl_n4096_l32(oracle):
     fr = oracle.frozen_bits_bb(4096, 2048, 0.0)
     llr, _, _ = frames.awgn_frames(4096, fr, 64, 1.5, seed=5, crc=8)
     _check_scl(oracle, 4096, 32, fr, llr)
+
+
+def test_scl32_config5_shard(oracle):
+    """Config 5 at its per-GPU shard size: 2^17 frames of N=4096 K=2048 SCL-32 (one of the
+    8 contiguous shards of the 2^20-frame batch), frames made on the device; a strided subset
+    is checked against the oracle (info, ok and path metrics bit for bit), every frame against
+    the transmitted information where the CRC passed."""
+    import torch
+    from antpolarcodes_amd._native import Encoder, Plan, bpsk_awgn_device, random_info_device
+    N, K, L, F = 4096, 2048, 32, 1 << 17
+    fr = oracle.frozen_bits_bb(N, K, 0.0)
+    info = torch.empty((F, K // 8), dtype=torch.uint8, device="cuda:0")
+    code = torch.empty((F, N // 8), dtype=torch.uint8, device="cuda:0")
+    llr = torch.empty((F, N), dtype=torch.float32, device="cuda:0")
+    random_info_device(info, K, seed=17)
+    Encoder(N, fr, crc=8, device=0).encode_device(info, code)
+    esn0 = 10 ** 0.15 * K / N  # Eb/N0 1.5 dB
+    bpsk_awgn_device(code, N, float(1 / np.sqrt(2 * esn0)), 23, llr)
+    del code
+    p = Plan(N, L, fr, crc=8, device=0)
+    out = torch.empty_like(info)
+    ok = torch.empty(F, dtype=torch.uint8, device="cuda:0")
+    met = torch.empty((F, L), dtype=torch.float32, device="cuda:0")
+    p.decode_device(llr, out, ok, met)
+    torch.cuda.synchronize()
+    okh = ok.cpu().numpy().astype(bool)
+    good = (out == info).all(dim=1).cpu().numpy()
+    assert okh.mean() > 0.9 and good[okh].mean() > 0.999
+    idx = np.arange(0, F, F // 48)
+    sub = llr[idx].cpu().numpy()
+    oi, ook, om, _, _ = oracle.scl_decode(N, L, fr, sub, crc=8, paths=True)
+    assert np.array_equal(out[idx].cpu().numpy(), oi)
+    assert np.array_equal(okh[idx].astype(np.uint8), ook)
+    assert np.array_equal(met[idx].cpu().numpy().view(np.uint32), om.view(np.uint32))
