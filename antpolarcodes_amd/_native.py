@@ -78,6 +78,8 @@ def lib():
         L.pcg_decode_i8_host.argtypes = [P, P, C.c_uint64, P, P, P]
         L.pcg_decode_f32.argtypes = [P, P, C.c_uint64, P, P, P, P]
         L.pcg_decode_f32_host.argtypes = [P, P, C.c_uint64, P, P, P]
+        L.pcg_decode_f32_soft.argtypes = [P, P, C.c_uint64, P, P, P, P]
+        L.pcg_decode_f32_soft_host.argtypes = [P, P, C.c_uint64, P, P, P]
         L.pcg_plan_describe.argtypes = [P, C.POINTER(PlanDesc)]
         L.pcg_plan_kernel_name.argtypes = [P]
         L.pcg_plan_kernel_name.restype = C.c_char_p
@@ -216,6 +218,26 @@ class Plan:
                                         None if ok is None else ok.ctypes.data,
                                         None if met is None else met.ctypes.data))
         return info, ok, met
+
+    def decode_soft_device(self, llr, info, ok, soft, stream=None):
+        """Fast-SSC float plans: decode and write the F x N soft codewords
+        (pcg_decode_f32_soft, Decoder::getSoftCodeword)."""
+        import torch
+        F = self._check_io(llr, info, ok, None, torch.float32)
+        _check_tensor("soft", soft, torch.float32, (F, self.N), self.device)
+        _check(lib().pcg_decode_f32_soft(self._h, _ptr(llr), F, _ptr(info), _ptr(ok), _ptr(soft),
+                                         _stream(stream, llr)))
+
+    def decode_soft_host(self, llr):
+        """Host arrays: returns (info, ok, soft codewords) (pcg_decode_f32_soft_host)."""
+        llr = np.ascontiguousarray(llr, dtype=np.float32).reshape(-1, self.N)
+        F = llr.shape[0]
+        info = np.zeros((F, self.kb), np.uint8)
+        ok = np.zeros(F, np.uint8)
+        soft = np.zeros((F, self.N), np.float32)
+        _check(lib().pcg_decode_f32_soft_host(self._h, llr.ctypes.data, F, info.ctypes.data, ok.ctypes.data,
+                                              soft.ctypes.data))
+        return info, ok, soft
 
     def decode_device_i8(self, llr, info, ok=None, metrics=None, stream=None):
         """int8 device frames (torch.int8 CUDA tensors F x N): pcg_decode_i8."""

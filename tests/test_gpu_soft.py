@@ -79,13 +79,17 @@ def test_kat_generic_leaves(oracle, kind, N):  # decodingtest.cpp:284-411
 def test_soft_codewords_bit_exact_vs_oracle(oracle):
     """Every Fast-SSC node kind at the root and inside BB codes, LLR families with ties,
     +-0 and wide ranges: the soft codeword equals the oracle's word for word."""
-    from antpolarcodes_amd._native import Plan
+    from antpolarcodes_amd._native import PCG_E_FROZEN, PcgError, Plan
     rng = np.random.default_rng(5)
     cases = [(N, fr) for N, fr in node_cover_sets()]
     for N in (64, 256, 1024):
         cases.append((N, oracle.frozen_bits_bb(N, N // 2, 0.0)))
     for N, fr in cases:
-        p = Plan(N, 1, fr, systematic=False, crc=0, device=0)
+        try:
+            p = Plan(N, 1, fr, systematic=False, crc=0, device=0)
+        except PcgError as e:  # frozen patterns the reference rejects (invalid_argument)
+            assert e.code == PCG_E_FROZEN
+            continue
         for kind in LLR_KINDS:
             llr = llr_kinds(rng, 16, N, kind)
             info, ok, soft = _decode_soft(p, llr)
@@ -97,15 +101,16 @@ def test_soft_codewords_bit_exact_vs_oracle(oracle):
 
 def _decode_soft(plan, llr):
     import torch
-    from antpolarcodes_amd._native import _check, lib
     F = llr.shape[0]
     d_llr = torch.from_numpy(np.ascontiguousarray(llr)).cuda()
     info = torch.zeros((F, plan.kb), dtype=torch.uint8, device="cuda")
     ok = torch.zeros(F, dtype=torch.uint8, device="cuda")
     soft = torch.zeros((F, plan.N), dtype=torch.float32, device="cuda")
-    _check(lib().pcg_decode_f32_soft(plan._h, d_llr.data_ptr(), F, info.data_ptr(), ok.data_ptr(),
-                                     soft.data_ptr(), torch.cuda.current_stream().cuda_stream))
+    plan.decode_soft_device(d_llr, info, ok, soft)
     torch.cuda.synchronize()
+    hi, hok, hs = plan.decode_soft_host(llr)  # the host-buffer entry point agrees
+    assert np.array_equal(hi, info.cpu().numpy()) and np.array_equal(hs.view(np.uint32),
+                                                                      soft.cpu().numpy().view(np.uint32))
     return info.cpu().numpy(), ok.cpu().numpy(), soft.cpu().numpy()
 
 
