@@ -119,7 +119,8 @@ const char* kernel_name(const pcg::PlanHost& h)
     if (h.L == 1) {
         if (h.fixed)
             return h.sc_kind == 0 ? "sccs_kernel" : "sc_char_kernel";
-        return h.sc_kind == 0 ? "scs_kernel" : "sc_kernel";
+        return h.sc_kind == 2 ? (h.scq_q == 8 ? "scq_kernel<8>" : h.scq_q == 32 ? "scq_kernel<32>" : "scq_kernel<16>")
+                              : (h.sc_kind == 0 ? "scs_kernel" : "sc_kernel");
     }
     const int i = __builtin_ctz(list_pow2(h.L)) - 1;
     return h.fixed ? sclc[i] : sclls[i];
@@ -197,7 +198,30 @@ static int plan_create_impl(pcg_plan** out,
         delete p;
         return fail(rc, err);
     }
-    if (fixed && L == 1 && p->host.sc_kind == 0 &&
+    if (fixed && L == 1 && p->host.sc_kind == 2)
+        p->host.sc_kind = 0; // the 8-bit decoder has no LDS-resident variant: lane-serial first
+    if (!fixed && L == 1 && p->host.sc_kind == 2) {
+        // LDS-resident Fast-SSC: Q lanes per codeword (PCG_SCQ_Q dev override), while a
+        // wave's state fits a CU and leaves room for several waves
+        uint32_t q = 16;
+        if (const char* e = getenv("PCG_SCQ_Q"))
+            q = (uint32_t)atoi(e);
+        bool v = true; // the root's children recomputed from the channel (half the LDS)
+        if (const char* e = getenv("PCG_SCQ_VIRT"))
+            v = e[0] != '0';
+        const uint32_t d = N <= 4096 ? pcg::scq_layout(N, q, v) : 0u;
+        if (d != 0) {
+            p->host.scq_q = q;
+            p->host.scq_virt = v ? 1 : 0;
+            p->wave_lds_floats = d;
+            p->scratch_floats = 0;
+        } else {
+            p->host.sc_kind = 0;
+        }
+    }
+    if (!fixed && L == 1 && p->host.sc_kind == 2) {
+        // (layout chosen above)
+    } else if (fixed && L == 1 && p->host.sc_kind == 0 &&
         pcg::sccs_layout(N, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats) == 0) {
         // lane-serial 8-bit Fast-SSC
     } else if (fixed && L == 1) {
@@ -253,7 +277,8 @@ static int plan_create_impl(pcg_plan** out,
     const auto& h = p->host;
     hipError_t e;
     if ((e = hipMalloc(&p->d_ops, 4 * std::max<size_t>(1, h.ops.size()))) != hipSuccess ||
-        (e = hipMalloc(&p->d_info_pos, 2 * (h.info_pos.size() + 2))) != hipSuccess ||
+        // info positions padded to whole 16-byte groups (scq_kernel.hip reads 8 at once)
+        (e = hipMalloc(&p->d_info_pos, 2 * (h.info_pos.size() + 16))) != hipSuccess ||
         (e = hipMalloc(&p->d_crc_m, 4 * (h.crc_m.size() + h.crc_rows.size() + 1))) != hipSuccess) {
         free_plan_device(p);
         delete p;
@@ -266,6 +291,8 @@ static int plan_create_impl(pcg_plan** out,
     } else if (h.fixed && h.L > 1) {
         p->wave_cap = pcg::sclc_wave_cap(h.L, p->wave_lds_floats, false);
         p->wave_cap_i8 = pcg::sclc_wave_cap(h.L, p->wave_lds_floats, true);
+    } else if (!h.fixed && h.L == 1 && h.sc_kind == 2) {
+        p->wave_cap = pcg::scq_wave_cap(h.scq_q, h.scq_virt != 0, p->wave_lds_floats);
     } else if (!h.fixed && h.L == 1 && h.sc_kind == 0) {
         p->wave_cap = pcg::scs_wave_cap(p->wave_lds_floats);
     } else if (!h.fixed && h.L > 1) {
@@ -535,6 +562,9 @@ static int decode_impl(pcg_plan* p,
             return rc;
         a.scratch = p->d_scratch;
         rc = pcg::launch_scl_char(a, s);
+    } else if (h.L == 1 && h.sc_kind == 2) {
+        a.units = (uint32_t)pcg::wave_units(F, 64 / h.scq_q, p->wave_cap);
+        rc = pcg::launch_scq(a, h.scq_q, h.scq_virt != 0, s);
     } else if (h.L == 1 && h.sc_kind == 0) {
         a.units = (uint32_t)pcg::wave_units(F, 64, p->wave_cap);
         if ((rc = grow_scratch(p, a.units, sizeof(float), s)) != 0)

@@ -114,6 +114,11 @@ uint64_t sclc_wave_cap(uint32_t L, uint32_t lds_dwords, bool i8);
 int scs_layout(uint32_t N, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratch_dwords);
 uint64_t scs_wave_cap(uint32_t lds_dwords);
 int launch_scs(const KernelArgs& a, hipStream_t stream);
+// LDS-resident Fast-SSC (scq_kernel.hip), Q lanes per codeword: LDS dwords per wave (0: does
+// not fit), wave cap, launch
+uint32_t scq_layout(uint32_t N, uint32_t Q, bool V);
+uint64_t scq_wave_cap(uint32_t Q, bool V, uint32_t lds_dwords);
+int launch_scq(const KernelArgs& a, uint32_t Q, bool V, hipStream_t stream);
 // lane-serial 8-bit Fast-SSC (sccs_kernel.hip), 64 codewords per wave
 int sccs_layout(uint32_t N, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratch_dwords);
 uint64_t sccs_wave_cap(uint32_t lds_dwords, bool i8);

@@ -305,7 +305,9 @@ int build_plan(PlanHost& p,
     p.fixed = fixed ? 1 : 0;
     {
         const char* k = getenv("PCG_SC_KERNEL"); // dev switch: "wave" = sc_kernel.hip
-        p.sc_kind = (k && std::string(k) == "wave") ? 1 : 0;
+        // "wave" = sc_kernel.hip, "scs" = lane-serial scs_kernel.hip, default: the float
+        // decoder's LDS-resident scq_kernel.hip where it fits (capi.cpp), else scs
+        p.sc_kind = (k && std::string(k) == "wave") ? 1 : ((k && std::string(k) == "scs") ? 0 : 2);
     }
     try {
         if (p.fixed && L == 1)

@@ -92,7 +92,9 @@ struct PlanHost {
     std::vector<int> node_types;    // pre-order census (op code of each node; 0 = internal)
     bool scl_st8 = true;            // emit lane-serial size-8 subtrees for SCL
     int fixed = 0;                  // 1: the reference's 8-bit decoders (FastSscFipChar / SclFipChar)
-    int sc_kind = 0;                // Fast-SSC kernel: 0 lane-serial (scs_kernel.hip), 1 one codeword per wave
+    int sc_kind = 0;  // Fast-SSC kernel: 2 = scq (LDS-resident), 0 = lane-serial, 1 = one codeword per wave
+    uint32_t scq_q = 16; // scq: lanes per codeword
+    int scq_virt = 1;     // scq: the root's children recomputed from the channel
 };
 
 // Returns 0, or a negative pcg.h error code with *err set.

@@ -158,8 +158,11 @@ def measure_traffic(args, kernel, frames):
     rocprof = shutil.which("rocprofv3")
     if not rocprof or not kernel:
         return None, "rocprofv3 not found" if not rocprof else "no kernel name"
+    # "sclls_kernel<8>" matches rocprof's "...sclls_kernel<8>(pcg::KernelArgs)" and
+    # "scq_kernel<16>" its "...scq_kernel<16, true, false>(...)": name + first template argument
     base = kernel.split("<")[0]
-    tmpl = kernel[len(base):]
+    targ = kernel[len(base) + 1:-1] if "<" in kernel else ""
+    pats = (f"{base}<{targ}>", f"{base}<{targ},") if targ else (base,)
     vals = {}
     with tempfile.TemporaryDirectory(prefix="pcg_traffic_", dir="/tmp") as td:
         for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -177,8 +180,7 @@ def measure_traffic(args, kernel, frames):
             if r.returncode != 0:
                 return None, f"rocprofv3 {ctr} pass failed (rc {r.returncode}): {r.stderr[-300:]}"
             per = [float(row["Counter_Value"]) for row in _counter_rows(od)
-                   if row.get("Counter_Name") == ctr and base in row.get("Kernel_Name", "")
-                   and (not tmpl or tmpl in row.get("Kernel_Name", ""))]
+                   if row.get("Counter_Name") == ctr and any(q in row.get("Kernel_Name", "") for q in pats)]
             if not per:
                 return None, f"no {ctr} rows for {kernel}"
             per.sort()
@@ -487,6 +489,9 @@ def main(argv=None):
                 tb = traffic["bytes_per_codeword"] * F
                 roof["traffic"] = tb
                 roof["traffic_bytes_per_codeword"] = traffic["bytes_per_codeword"]
+                if "read_bytes_per_launch" in traffic:
+                    roof["traffic_read_bytes_per_codeword"] = traffic["read_bytes_per_launch"] / F
+                    roof["traffic_write_bytes_per_codeword"] = traffic["write_bytes_per_launch"] / F
                 roof["traffic_frac"] = tb / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if kern_ms > 0 else None
                 roof["traffic_source"] = traffic["source"]
             else:
