@@ -203,12 +203,22 @@ static int plan_create_impl(pcg_plan** out,
     if (!fixed && L == 1 && p->host.sc_kind == 2) {
         // LDS-resident Fast-SSC: Q lanes per codeword (PCG_SCQ_Q dev override), while a
         // wave's state fits a CU and leaves room for several waves
-        uint32_t q = 16;
+        uint32_t q = 8;
         if (const char* e = getenv("PCG_SCQ_Q"))
             q = (uint32_t)atoi(e);
         bool v = true; // the root's children recomputed from the channel (half the LDS)
         if (const char* e = getenv("PCG_SCQ_VIRT"))
             v = e[0] != '0';
+        // ... only F / G / G0 / ROne read them (leaves and fused size-16 ops read stored stages)
+        const auto& fo = p->host.ops_fused;
+        for (size_t k = 0; k < fo.size(); ++k) {
+            const uint32_t c = pcg::op_code(fo[k]), st = pcg::op_stage(fo[k]);
+            if (st == p->host.log2N - 1 && c != pcg::OP_F && c != pcg::OP_G && c != pcg::OP_G0 && c != pcg::OP_RONE &&
+                c != pcg::OP_COMB && c != pcg::OP_COPY0)
+                v = false;
+            if (c == pcg::OP_Q16 || c == pcg::OP_Q16R)
+                ++k; // descriptor word
+        }
         const uint32_t d = N <= 4096 ? pcg::scq_layout(N, q, v) : 0u;
         if (d != 0) {
             p->host.scq_q = q;
@@ -276,7 +286,7 @@ static int plan_create_impl(pcg_plan** out,
     }
     const auto& h = p->host;
     hipError_t e;
-    if ((e = hipMalloc(&p->d_ops, 4 * std::max<size_t>(1, h.ops.size()))) != hipSuccess ||
+    if ((e = hipMalloc(&p->d_ops, 4 * std::max<size_t>(1, h.ops.size() + h.ops_fused.size()))) != hipSuccess ||
         // info positions padded to whole 16-byte groups (scq_kernel.hip reads 8 at once)
         (e = hipMalloc(&p->d_info_pos, 2 * (h.info_pos.size() + 16))) != hipSuccess ||
         (e = hipMalloc(&p->d_crc_m, 4 * (h.crc_m.size() + h.crc_rows.size() + 1))) != hipSuccess) {
@@ -308,6 +318,8 @@ static int plan_create_impl(pcg_plan** out,
         }
     }
     if ((e = hipMemcpy(p->d_ops, h.ops.data(), 4 * h.ops.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+        (!h.ops_fused.empty() && (e = hipMemcpy(p->d_ops + h.ops.size(), h.ops_fused.data(), 4 * h.ops_fused.size(),
+                                                hipMemcpyHostToDevice)) != hipSuccess) ||
         (!h.info_pos.empty() &&
          (e = hipMemcpy(p->d_info_pos, h.info_pos.data(), 2 * h.info_pos.size(), hipMemcpyHostToDevice)) !=
              hipSuccess) ||
@@ -564,6 +576,8 @@ static int decode_impl(pcg_plan* p,
         rc = pcg::launch_scl_char(a, s);
     } else if (h.L == 1 && h.sc_kind == 2) {
         a.units = (uint32_t)pcg::wave_units(F, 64 / h.scq_q, p->wave_cap);
+        a.ops = p->d_ops + h.ops.size(); // the fused schedule (plan.cpp fuse_sc16)
+        a.nops = (uint32_t)h.ops_fused.size();
         rc = pcg::launch_scq(a, h.scq_q, h.scq_virt != 0, s);
     } else if (h.L == 1 && h.sc_kind == 0) {
         a.units = (uint32_t)pcg::wave_units(F, 64, p->wave_cap);

@@ -124,6 +124,36 @@ void sc_emit(PlanHost& p, const std::vector<uint32_t>& f, uint32_t n, uint32_t o
     p.ops.push_back(mkop(OP_COMB, n, off));
 }
 
+// scq_kernel.hip's schedule: [F 4 o][leaf 3 o][G 4 o][leaf 3 o+8][COMB 4 o] -> [Q16 4 o][desc],
+// [F 4 o][leaf 3 o][RONE 4 o] -> [Q16R 4 o][desc] (size-8 leaves of the Fast-SSC tree).
+void fuse_sc16(PlanHost& p)
+{
+    const auto& v = p.ops;
+    auto is8 = [&](size_t k, uint32_t o) {
+        return k < v.size() && op_code(v[k]) >= OP_L_R0 && op_code(v[k]) <= OP_L_ZSPC && op_stage(v[k]) == 3 &&
+               op_off(v[k]) == o;
+    };
+    auto is = [&](size_t k, uint32_t code, uint32_t o) {
+        return k < v.size() && op_code(v[k]) == code && op_stage(v[k]) == 4 && op_off(v[k]) == o;
+    };
+    p.ops_fused.clear();
+    for (size_t k = 0; k < v.size();) {
+        const uint32_t o = op_off(v[k]);
+        if (is(k, OP_F, o) && is8(k + 1, o) && is(k + 2, OP_G, o) && is8(k + 3, o + 8) && is(k + 4, OP_COMB, o)) {
+            p.ops_fused.push_back(mkop(OP_Q16, 16, o));
+            p.ops_fused.push_back(op_code(v[k + 1]) | (op_code(v[k + 3]) << 8));
+            k += 5;
+        } else if (is(k, OP_F, o) && is8(k + 1, o) && is(k + 2, OP_RONE, o)) {
+            p.ops_fused.push_back(mkop(OP_Q16R, 16, o));
+            p.ops_fused.push_back(op_code(v[k + 1]));
+            k += 3;
+        } else {
+            p.ops_fused.push_back(v[k]);
+            ++k;
+        }
+    }
+}
+
 // SCL classification of a small node (n <= 4) as an ST8 descriptor kind.
 uint32_t scl_small_kind(const std::vector<uint32_t>& f, uint32_t n, PlanHost& p, uint32_t* sub)
 {
@@ -315,7 +345,10 @@ int build_plan(PlanHost& p,
         else if (p.fixed)
             scl_char_emit(p, p.frozen, N, 0);
         else if (L == 1)
+        {
             sc_emit(p, p.frozen, N, 0);
+            fuse_sc16(p);
+        }
         else
             scl_emit(p, p.frozen, N, 0);
     } catch (Err& e) {

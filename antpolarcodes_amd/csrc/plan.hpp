@@ -41,6 +41,11 @@ enum OpCode : uint32_t {
     OP_L_REPR1 = 25, // :718-739
     OP_L_ZSPC8 = 26, // :556-565
     OP_L_ZSPC = 27,  // :503-546 (reproduces the reference's right-half output, Q1)
+    // scq_kernel.hip only (PlanHost::ops_fused): a size-16 RateRNode whose children are size-8
+    // leaves (F, leaf, G, leaf, COMB) or a size-16 ROneNode over a size-8 leaf (F, leaf,
+    // RONE), run in registers as one op; the next word holds the leaf codes (left | right << 8)
+    OP_Q16 = 28,
+    OP_Q16R = 29,
     // SCL leaves (scl_avx_float.cpp)
     OP_S_R0 = 40,  // :316-337
     OP_S_R1 = 41,  // :353-413
@@ -84,6 +89,7 @@ struct PlanHost {
     int crc_kind = 0;
     std::vector<uint32_t> frozen;
     std::vector<uint32_t> ops;      // flattened schedule
+    std::vector<uint32_t> ops_fused; // Fast-SSC float: `ops` with size-16 leaf pairs fused (OP_Q16/Q16R)
     std::vector<uint16_t> info_pos; // K non-frozen positions, ascending (bitcontainer.cpp:68-84)
     std::vector<uint32_t> crc_m;    // K affine syndrome columns
     uint32_t crc_c0 = 0;            // syndrome of the all-zero message

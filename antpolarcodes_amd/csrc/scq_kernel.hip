@@ -68,16 +68,20 @@ PCG_DEV uint32_t or8(uint32_t v)
 // kernels -- a child of the root recomputed from the channel wherever it is read: F(y_i,
 // y_i+N/2) (mode 1), G(y_i, y_i+N/2, bit_i) with the codeword's left-half bits (mode 2),
 // y_i + y_i+N/2 below a ZeroRNode root (mode 3).  The mode is wave-uniform.
-struct Src {
+// Two source types, so that code reading the stored stages never carries the recompute
+// path (register pressure): PSrc (LDS stage or channel frame), VSrc (recomputed child).
+struct PSrc {
     const float* p;
+    PCG_DEV float4 ld(uint32_t c) const { return reinterpret_cast<const float4*>(p)[c]; }
+    PCG_DEV float at(uint32_t i) const { return p[i]; }
+};
+struct VSrc {
     const float* y;
     const uint32_t* row;
     uint32_t half;
     uint32_t mode;
     PCG_DEV float4 ld(uint32_t c) const
     {
-        if (mode == 0)
-            return reinterpret_cast<const float4*>(p)[c];
         const float4 a = reinterpret_cast<const float4*>(y)[c], b = reinterpret_cast<const float4*>(y + half)[c];
         if (mode == 1)
             return q_f(a, b);
@@ -87,8 +91,6 @@ struct Src {
     }
     PCG_DEV float at(uint32_t i) const
     {
-        if (mode == 0)
-            return p[i];
         const float a = y[i], b = y[i + half];
         if (mode == 1)
             return polar_f(a, b);
@@ -108,13 +110,16 @@ struct Cw {
     uint32_t virt;  // 1: the root's children are recomputed (Src modes 1-3), never stored
     uint32_t root;  // Src mode of the recomputed children
 
-    PCG_DEV Src src(uint32_t s) const
+    // stage s as a source: f(PSrc) for stored stages and the channel, f(VSrc) for a
+    // recomputed child of the root
+    PCG_DEV PSrc psrc(uint32_t s) const { return PSrc{ s == top ? y : alpha + (1u << s) }; }
+    template <typename Fn>
+    PCG_DEV void with_src(uint32_t s, Fn&& f) const
     {
-        if (s == top)
-            return Src{ y, y, row, N / 2, 0u };
         if (virt && s == top - 1)
-            return Src{ nullptr, y, row, N / 2, root };
-        return Src{ alpha + (1u << s), y, row, N / 2, 0u };
+            f(VSrc{ y, row, N / 2, root });
+        else
+            f(PSrc{ s == top ? y : alpha + (1u << s) });
     }
     PCG_DEV uint32_t nib(uint32_t pos) const { return (row[pos >> 5] >> (pos & 31u)) & 0xfu; }
     // positions [o, o+c) (c <= 32, inside one word) := v      (single lane)
@@ -179,7 +184,8 @@ PCG_DEV uint32_t spc4_q(const float (&v)[4])
 
 // 8 lane partial sums of the reference (lanes from +0.0, chunks of 8 ascending; n < 8
 // padded with +0.0), serial on one lane (avxconvenience.h:256-272, avx_float.h:238-250)
-PCG_DEV void lane_sums_q(const Src& src, uint32_t n, float (&s)[8])
+template <typename SRC>
+PCG_DEV void lane_sums_q(const SRC& src, uint32_t n, float (&s)[8])
 {
 #pragma unroll
     for (int j = 0; j < 8; ++j)
@@ -204,8 +210,8 @@ PCG_DEV void lane_sums_q(const Src& src, uint32_t n, float (&s)[8])
 
 // Leaf kinds run on the group's first lane with the reference's scalar loops
 // (fastssc_avx_float.cpp:303-792, oracle/polar_oracle.c sc_leaf).
-template <int Q>
-PCG_DEV void serial_leaf(const Cw<Q>& w, uint32_t code, const Src& src, uint32_t n, uint32_t o)
+template <int Q, typename SRC>
+PCG_DEV void serial_leaf(const Cw<Q>& w, uint32_t code, const SRC& src, uint32_t n, uint32_t o)
 {
     switch (code) {
     case OP_L_REP: { // n < 8 (larger repetition leaves run group-parallel)
@@ -418,8 +424,8 @@ PCG_DEV void serial_leaf(const Cw<Q>& w, uint32_t code, const Src& src, uint32_t
 // The reference's 8 AVX lane sums s_j (each from +0.0, chunks of 8 ascending; n < 8
 // padded with +0.0): group lane j < 8 accumulates s_j in the reference's order, then every
 // lane of the group receives all eight.
-template <int Q>
-PCG_DEV void grp_lane_sums(const Cw<Q>& w, const Src& src, uint32_t n, float (&s)[8])
+template <int Q, typename SRC>
+PCG_DEV void grp_lane_sums(const Cw<Q>& w, const SRC& src, uint32_t n, float (&s)[8])
 {
     float acc = 0.0f;
     if (w.sub < 8) {
@@ -444,8 +450,8 @@ PCG_DEV void fill_any(const Cw<Q>& w, uint32_t o, uint32_t n, uint32_t pat)
 
 // Leaf kinds whose reductions follow the 8 AVX lanes, run on the group (the reference's
 // loops per AVX lane on group lanes 0..7; the tail math, identical in every lane)
-template <int Q>
-PCG_DEV bool grp_leaf(const Cw<Q>& w, uint32_t code, const Src& src, uint32_t n, uint32_t o)
+template <int Q, typename SRC>
+PCG_DEV bool grp_leaf(const Cw<Q>& w, uint32_t code, const SRC& src, uint32_t n, uint32_t o)
 {
     switch (code) {
     case OP_L_DREP: { // DoubleRepetitionDecoder :303-332
@@ -590,11 +596,10 @@ PCG_DEV bool grp_leaf(const Cw<Q>& w, uint32_t code, const Src& src, uint32_t n,
     }
 }
 
-template <int Q>
-PCG_DEV void leaf_q(const Cw<Q>& w, uint32_t code, uint32_t s, uint32_t o)
+template <int Q, typename SRC>
+PCG_DEV void leaf_body(const Cw<Q>& w, uint32_t code, const SRC& src, uint32_t s, uint32_t o)
 {
     const uint32_t n = 1u << s;
-    const Src src = w.src(s);
     if (code == OP_L_R0) { // RateZeroDecoder: +INF bits
         w.fill(o, n, 0u);
         return;
@@ -656,16 +661,151 @@ PCG_DEV void leaf_q(const Cw<Q>& w, uint32_t code, uint32_t s, uint32_t o)
         serial_leaf<Q>(w, code, src, n, o);
 }
 
-// F / G / G0 from stage s into stage s-1, or the fused right rate-1 of ROneNode (:205-219)
+// (leaves never read a recomputed child: the host stores the children of a root with a
+// leaf child, capi.cpp)
 template <int Q>
-PCG_DEV void inner_q(Cw<Q>& w, uint32_t code, uint32_t s, uint32_t o)
+PCG_DEV void leaf_q(const Cw<Q>& w, uint32_t code, uint32_t s, uint32_t o)
+{
+    leaf_body<Q>(w, code, w.psrc(s), s, o);
+}
+
+// A size-8 Fast-SSC leaf on 8 LLRs in registers: the 8 output sign bits (bit i = position i).
+// Exactly the reference's n = 8 arithmetic (lane sums of one chunk are +0.0 + x_j).
+PCG_DEV uint32_t leaf8_bits(uint32_t code, const float (&x)[8])
+{
+    uint32_t sg = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        sg |= (fbits(x[j]) >> 31) << j;
+    switch (code) {
+    case OP_L_R0:
+        return 0u;
+    case OP_L_R1:
+        return sg;
+    case OP_L_REP: { // :273-287
+        float S = 0.0f + x[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j)
+            S = S + (0.0f + x[j]);
+        return (fbits(S) >> 31) ? 0xffu : 0u;
+    }
+    case OP_L_SPC: { // :342-373, n = 8: argmin lowest index, parity of all signs
+        uint32_t par = 0, m = 0;
+        float mv = __builtin_inff();
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            par ^= fbits(x[j]);
+            const float a = fabs_(x[j]);
+            if (a < mv) {
+                mv = a;
+                m = (uint32_t)j;
+            }
+        }
+        return sg ^ ((par >> 31) << m);
+    }
+    case OP_L_DREP: { // :303-332, n = 8
+        const float ev = ((0.0f + x[0]) + (0.0f + x[4])) + ((0.0f + x[2]) + (0.0f + x[6]));
+        const float od = ((0.0f + x[1]) + (0.0f + x[5])) + ((0.0f + x[3]) + (0.0f + x[7]));
+        const uint32_t e = fbits(ev) >> 31, d = fbits(od) >> 31;
+        return (e ? 0x55u : 0u) | (d ? 0xaau : 0u);
+    }
+    case OP_L_DSPC8: { // :473-488 (multi-flip on ties)
+        float av[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            av[j] = fabs_(x[j]);
+        const float ce = minps(minps(av[0], av[4]), minps(av[2], av[6]));
+        const float co = minps(minps(av[1], av[5]), minps(av[3], av[7]));
+        const uint32_t pe = (fbits(x[0]) ^ fbits(x[2]) ^ fbits(x[4]) ^ fbits(x[6])) >> 31;
+        const uint32_t po = (fbits(x[1]) ^ fbits(x[3]) ^ fbits(x[5]) ^ fbits(x[7])) >> 31;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const bool ev = (j & 1) == 0;
+            const uint32_t hit = av[j] == (ev ? ce : co) ? (ev ? pe : po) : 0u;
+            acc |= ((fbits(x[j]) >> 31) ^ hit) << j;
+        }
+        return acc;
+    }
+    case OP_L_ZSPC8: { // :556-565
+        const float v[4] = { x[0] + x[4], x[1] + x[5], x[2] + x[6], x[3] + x[7] };
+        const uint32_t ob = spc4_q(v);
+        return ob | (ob << 4);
+    }
+    case OP_L_TYPE5:   // :762-792, n = 8 (lane sums of one chunk)
+    case OP_L_REPR1: { // :718-739
+        float l[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            l[j] = code == OP_L_TYPE5 ? 0.0f + x[j] : x[j];
+        float r[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            r[k] = polar_f(l[k], l[k + 4]);
+        const float R = (r[0] + r[1]) + (r[2] + r[3]);
+        float g[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            g[k] = polar_g(l[k], l[k + 4], sgn(R));
+        uint32_t ob;
+        if (code == OP_L_TYPE5) {
+            ob = spc4_q(g);
+        } else {
+            ob = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                ob |= (fbits(g[k]) >> 31) << k;
+        }
+        return (ob ^ ((fbits(R) >> 31) ? 0xfu : 0u)) | (ob << 4);
+    }
+    default:
+        return 0u;
+    }
+}
+
+// OP_Q16 / OP_Q16R: a size-16 node over size-8 leaves in registers on the codeword's first
+// lane -- RateRNode (:148-155: F, left leaf, G, right leaf, Combine) or ROneNode
+// (:198-219: F, left leaf, fused right rate-1).  16 LLRs in, 16 bits out.
+template <int Q, typename SRC>
+PCG_DEV void q16_body(const Cw<Q>& w, const SRC& src, uint32_t code, uint32_t o, uint32_t desc)
+{
+    const float4 c0 = src.ld(0), c1 = src.ld(1), c2 = src.ld(2), c3 = src.ld(3);
+    const float a[8] = { c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w };
+    const float b[8] = { c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w };
+    float l[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        l[i] = polar_f(a[i], b[i]);
+    const uint32_t bl = leaf8_bits(desc & 0xffu, l);
+    float r[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        r[i] = polar_g(a[i], b[i], ((bl >> i) & 1u) << 31);
+    uint32_t br;
+    if (code == OP_Q16) {
+        br = leaf8_bits((desc >> 8) & 0xffu, r);
+    } else { // right rate-1: bits = signs of r; left := left ^ right
+        br = 0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            br |= (fbits(r[i]) >> 31) << i;
+    }
+    w.put(o, 16, (bl ^ br) | (br << 8));
+}
+
+template <int Q>
+PCG_DEV void q16(const Cw<Q>& w, uint32_t code, uint32_t o, uint32_t desc)
+{
+    if (w.sub != 0)
+        return;
+    q16_body<Q>(w, w.psrc(4), code, o, desc);
+}
+
+// F / G / G0 from stage s into stage s-1, or the fused right rate-1 of ROneNode (:205-219)
+template <int Q, typename SRC>
+PCG_DEV void inner_body(const Cw<Q>& w, const SRC& src, uint32_t code, uint32_t s, uint32_t o)
 {
     const uint32_t h = 1u << (s - 1);
-    if (w.virt && s == w.top && code != OP_RONE) { // the root's children: recomputed where read
-        w.root = code == OP_F ? 1u : (code == OP_G ? 2u : 3u);
-        return;
-    }
-    const Src src = w.src(s);
     if (h < 4) { // h = 1, 2: one lane, scalar
         if (w.sub != 0)
             return;
@@ -704,20 +844,6 @@ PCG_DEV void inner_q(Cw<Q>& w, uint32_t code, uint32_t s, uint32_t o)
     }
     float4* dst = reinterpret_cast<float4*>(w.alpha + h);
     uint32_t c = w.sub;
-    for (; c + 3 * Q < hq; c += 4 * Q) { // four chunks in flight (all loads issued first)
-        float4 av[4], bv[4];
-#pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
-            av[q] = src.ld(c + q * Q);
-            bv[q] = src.ld(c + q * Q + hq);
-        }
-#pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
-            const uint32_t cq = c + q * Q;
-            dst[cq] = code == OP_F ? q_f(av[q], bv[q])
-                                   : (code == OP_G ? q_g(av[q], bv[q], w.nib(o + 4u * cq)) : q_add(av[q], bv[q]));
-        }
-    }
     for (; c + Q < hq; c += 2 * Q) { // two chunks in flight
         const float4 a0 = src.ld(c), b0 = src.ld(c + hq), a1 = src.ld(c + Q), b1 = src.ld(c + Q + hq);
         if (code == OP_F) {
@@ -735,6 +861,16 @@ PCG_DEV void inner_q(Cw<Q>& w, uint32_t code, uint32_t s, uint32_t o)
         const float4 a0 = src.ld(c), b0 = src.ld(c + hq);
         dst[c] = code == OP_F ? q_f(a0, b0) : (code == OP_G ? q_g(a0, b0, w.nib(o + 4u * c)) : q_add(a0, b0));
     }
+}
+
+template <int Q>
+PCG_DEV void inner_q(Cw<Q>& w, uint32_t code, uint32_t s, uint32_t o)
+{
+    if (w.virt && s == w.top && code != OP_RONE) { // the root's children: recomputed where read
+        w.root = code == OP_F ? 1u : (code == OP_G ? 2u : 3u);
+        return;
+    }
+    w.with_src(s, [&](const auto& src) { inner_body<Q>(w, src, code, s, o); });
 }
 
 // COMB (bit[o+i] ^= bit[o+h+i]) / COPY0 (bit[o+i] = bit[o+h+i])
@@ -759,7 +895,7 @@ PCG_DEV void bits_q(const Cw<Q>& w, uint32_t code, uint32_t s, uint32_t o)
 // PROF (development aid, PCG_OPPROF=1): s_memtime cycles and counts per op code in
 // a.prof[2 * code], a.prof[2 * code + 1], kept in LDS and flushed once per wave
 template <int Q, bool V, bool PROF>
-__global__ void __launch_bounds__(64) scq_kernel(KernelArgs a)
+__global__ void __launch_bounds__(64, 4) scq_kernel(KernelArgs a)
 {
     constexpr uint32_t G = 64 / Q;
     extern __shared__ float smem_q[];
@@ -790,7 +926,12 @@ __global__ void __launch_bounds__(64) scq_kernel(KernelArgs a)
             const uint32_t op = nxt; // the next schedule word is loaded while this op runs
             nxt = ld_const(a.ops, k + 1 < a.nops ? k + 1 : k);
             const uint32_t code = op_code(op), s = op_stage(op), o = op_off(op);
-            if (code >= OP_L_R0)
+            if (code == OP_Q16 || code == OP_Q16R) {
+                const uint32_t desc = nxt; // the descriptor word follows
+                ++k;
+                nxt = ld_const(a.ops, k + 1 < a.nops ? k + 1 : k);
+                q16<Q>(w, code, o, desc);
+            } else if (code >= OP_L_R0)
                 leaf_q<Q>(w, code, s, o);
             else if (code == OP_COMB || code == OP_COPY0)
                 bits_q<Q>(w, code, s, o);
