@@ -203,7 +203,7 @@ static int plan_create_impl(pcg_plan** out,
     if (!fixed && L == 1 && p->host.sc_kind == 2) {
         // LDS-resident Fast-SSC: Q lanes per codeword (PCG_SCQ_Q dev override), while a
         // wave's state fits a CU and leaves room for several waves
-        uint32_t q = 8;
+        uint32_t q = 16;
         if (const char* e = getenv("PCG_SCQ_Q"))
             q = (uint32_t)atoi(e);
         bool v = true; // the root's children recomputed from the channel (half the LDS)
@@ -212,7 +212,7 @@ static int plan_create_impl(pcg_plan** out,
         // ... only F / G / G0 / ROne read them (leaves and fused size-16 ops read stored stages)
         const auto& fo = p->host.ops_fused;
         for (size_t k = 0; k < fo.size(); ++k) {
-            const uint32_t c = pcg::op_code(fo[k]), st = pcg::op_stage(fo[k]);
+            const uint32_t c = pcg::op_code(fo[k]), st = pcg::op_stage(fo[k]) & 15u;
             if (st == p->host.log2N - 1 && c != pcg::OP_F && c != pcg::OP_G && c != pcg::OP_G0 && c != pcg::OP_RONE &&
                 c != pcg::OP_COMB && c != pcg::OP_COPY0)
                 v = false;

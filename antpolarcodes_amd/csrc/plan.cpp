@@ -136,21 +136,44 @@ void fuse_sc16(PlanHost& p)
     auto is = [&](size_t k, uint32_t code, uint32_t o) {
         return k < v.size() && op_code(v[k]) == code && op_stage(v[k]) == 4 && op_off(v[k]) == o;
     };
-    p.ops_fused.clear();
+    std::vector<uint32_t> out;
     for (size_t k = 0; k < v.size();) {
         const uint32_t o = op_off(v[k]);
         if (is(k, OP_F, o) && is8(k + 1, o) && is(k + 2, OP_G, o) && is8(k + 3, o + 8) && is(k + 4, OP_COMB, o)) {
-            p.ops_fused.push_back(mkop(OP_Q16, 16, o));
-            p.ops_fused.push_back(op_code(v[k + 1]) | (op_code(v[k + 3]) << 8));
+            out.push_back(mkop(OP_Q16, 16, o));
+            out.push_back(op_code(v[k + 1]) | (op_code(v[k + 3]) << 8));
             k += 5;
         } else if (is(k, OP_F, o) && is8(k + 1, o) && is(k + 2, OP_RONE, o)) {
-            p.ops_fused.push_back(mkop(OP_Q16R, 16, o));
-            p.ops_fused.push_back(op_code(v[k + 1]));
+            out.push_back(mkop(OP_Q16R, 16, o));
+            out.push_back(op_code(v[k + 1]));
             k += 3;
         } else {
-            p.ops_fused.push_back(v[k]);
+            out.push_back(v[k]);
             ++k;
         }
+    }
+    // Second pass: a parent's COMB right after the last op of its right child's subtree is
+    // folded into that op as a count of combine levels in the stage byte (stage | levels << 4):
+    // after the op, the kernel applies COMB at stages s+1 .. s+levels going up the right
+    // spine.  `end` tracks the subtree each emitted op completes.
+    p.ops_fused.clear();
+    size_t last = SIZE_MAX;           // index of the last op word (not a descriptor)
+    uint32_t end_s = 0, end_o = 0;    // the subtree it completes
+    for (size_t k = 0; k < out.size(); ++k) {
+        const uint32_t w = out[k], c = op_code(w), s = op_stage(w), o = op_off(w);
+        if (c == OP_COMB && last != SIZE_MAX && end_s + 1 == s && end_o == o + (1u << (s - 1)) &&
+            (op_stage(p.ops_fused[last]) >> 4) < 15) {
+            p.ops_fused[last] += 1u << 12; // one more level (bits 12..15 of the word)
+            end_s = s;
+            end_o = o;
+            continue;
+        }
+        last = p.ops_fused.size();
+        p.ops_fused.push_back(w);
+        end_s = s;
+        end_o = o;
+        if (c == OP_Q16 || c == OP_Q16R)
+            p.ops_fused.push_back(out[++k]); // descriptor
     }
 }
 

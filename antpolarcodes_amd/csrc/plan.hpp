@@ -43,7 +43,9 @@ enum OpCode : uint32_t {
     OP_L_ZSPC = 27,  // :503-546 (reproduces the reference's right-half output, Q1)
     // scq_kernel.hip only (PlanHost::ops_fused): a size-16 RateRNode whose children are size-8
     // leaves (F, leaf, G, leaf, COMB) or a size-16 ROneNode over a size-8 leaf (F, leaf,
-    // RONE), run in registers as one op; the next word holds the leaf codes (left | right << 8)
+    // RONE), run in registers as one op; the next word holds the leaf codes (left | right << 8).
+    // In ops_fused the stage byte also carries, in its high nibble, the number of parent
+    // COMB levels folded into the op (plan.cpp fuse_sc16).
     OP_Q16 = 28,
     OP_Q16R = 29,
     // SCL leaves (scl_avx_float.cpp)

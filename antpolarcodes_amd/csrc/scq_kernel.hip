@@ -925,7 +925,8 @@ __global__ void __launch_bounds__(64, 4) scq_kernel(KernelArgs a)
         for (uint32_t k = 0; k < a.nops; ++k) {
             const uint32_t op = nxt; // the next schedule word is loaded while this op runs
             nxt = ld_const(a.ops, k + 1 < a.nops ? k + 1 : k);
-            const uint32_t code = op_code(op), s = op_stage(op), o = op_off(op);
+            const uint32_t code = op_code(op), s = op_stage(op) & 15u, o = op_off(op);
+            const uint32_t up = op_stage(op) >> 4; // parent COMB levels folded into this op
             if (code == OP_Q16 || code == OP_Q16R) {
                 const uint32_t desc = nxt; // the descriptor word follows
                 ++k;
@@ -937,6 +938,11 @@ __global__ void __launch_bounds__(64, 4) scq_kernel(KernelArgs a)
                 bits_q<Q>(w, code, s, o);
             else
                 inner_q<Q>(w, code, s, o);
+            // the folded parent COMBs, up the right spine: child (sc, oc) -> parent (sc+1, oc - 2^sc)
+            for (uint32_t l = 0, sc = s, oc = o; l < up; ++l, oc -= 1u << sc, ++sc) {
+                wsync();
+                bits_q<Q>(w, OP_COMB, sc + 1, oc - (1u << sc));
+            }
             wsync();
             if constexpr (PROF) {
                 const uint64_t t1 = __builtin_amdgcn_s_memtime();

@@ -173,12 +173,17 @@ def measure_traffic(args, kernel, frames):
             env = dict(os.environ, TMPDIR="/tmp")
             for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
                 env.pop(k, None)
+            # own process group, so a pass that overruns is killed with the application it profiles
+            pr = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env,
+                                  start_new_session=True)
             try:
-                r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+                _, err = pr.communicate(timeout=240)
             except subprocess.TimeoutExpired:
+                os.killpg(pr.pid, 9)
+                pr.communicate()
                 return None, f"rocprofv3 {ctr} pass timed out"
-            if r.returncode != 0:
-                return None, f"rocprofv3 {ctr} pass failed (rc {r.returncode}): {r.stderr[-300:]}"
+            if pr.returncode != 0:
+                return None, f"rocprofv3 {ctr} pass failed (rc {pr.returncode}): {err[-300:]}"
             per = [float(row["Counter_Value"]) for row in _counter_rows(od)
                    if row.get("Counter_Name") == ctr and any(q in row.get("Kernel_Name", "") for q in pats)]
             if not per:

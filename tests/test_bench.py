@@ -75,7 +75,7 @@ def test_device_decode_rejects_bad_tensors():
     with pytest.raises(ValueError, match="contiguous"):
         p.decode_device(torch.zeros((128, 4)).t(), info)
     assert p.kernel_name() == "sclls_kernel<8>"
-    assert Plan(128, 1, fr, device=-1).kernel_name() == "scq_kernel<8>"
+    assert Plan(128, 1, fr, device=-1).kernel_name() == "scq_kernel<16>"
     assert Plan(128, 1, fr, device=-1, fixed=True).kernel_name() == "sccs_kernel"
     assert Plan(128, 32, fr, device=-1, fixed=True).kernel_name() == "scl_char_kernel<32>"
     np.testing.assert_equal(p.kb, 8)
