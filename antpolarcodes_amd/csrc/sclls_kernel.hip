@@ -138,9 +138,21 @@ PCG_DEV float4 f4_g(const float4& a, const float4& b, uint32_t wb)
                        polar_g(a.z, b.z, ((wb >> 2) & 1u) << 31), polar_g(a.w, b.w, ((wb >> 3) & 1u) << 31));
 }
 
+// Channel loads (dev experiment -DPCG_SCL_NT_CHAN: non-temporal, keeping the frames out of L2)
+PCG_DEV float4 chan_ld(const float* y, uint32_t c)
+{
+#ifdef PCG_SCL_NT_CHAN
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(y) + c);
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return reinterpret_cast<const float4*>(y)[c];
+#endif
+}
+
 struct ChSt { // the channel LLRs of the lane's own codeword (stage top)
     const float* y;
-    PCG_DEV float4 ld(uint32_t c, uint32_t) const { return reinterpret_cast<const float4*>(y)[c]; }
+    PCG_DEV float4 ld(uint32_t c, uint32_t) const { return chan_ld(y, c); }
 };
 template <bool LEFT>
 struct RootSt { // stage top-1, left or right child of the root
@@ -149,8 +161,8 @@ struct RootSt { // stage top-1, left or right child of the root
     uint32_t hq1;        // N/8 chunks: distance of y_j+N/2
     PCG_DEV float4 ld(uint32_t c, uint32_t) const
     {
-        const float4 a = reinterpret_cast<const float4*>(y)[c];
-        const float4 b = reinterpret_cast<const float4*>(y)[c + hq1];
+        const float4 a = chan_ld(y, c);
+        const float4 b = chan_ld(y, c + hq1);
         if (LEFT)
             return f4_f(a, b);
         const uint32_t i = 4u * c;
