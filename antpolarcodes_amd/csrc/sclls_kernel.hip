@@ -138,17 +138,10 @@ PCG_DEV float4 f4_g(const float4& a, const float4& b, uint32_t wb)
                        polar_g(a.z, b.z, ((wb >> 2) & 1u) << 31), polar_g(a.w, b.w, ((wb >> 3) & 1u) << 31));
 }
 
-// Channel loads (dev experiment -DPCG_SCL_NT_CHAN: non-temporal, keeping the frames out of L2)
-PCG_DEV float4 chan_ld(const float* y, uint32_t c)
-{
-#ifdef PCG_SCL_NT_CHAN
-    typedef float v4f __attribute__((ext_vector_type(4)));
-    const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(y) + c);
-    return make_float4(v.x, v.y, v.z, v.w);
-#else
-    return reinterpret_cast<const float4*>(y)[c];
-#endif
-}
+// Channel loads.  (Measured round 2: non-temporal loads here -- frames kept out of L2 to
+// leave it to the stage slab -- raise traffic to 330 KB/cw and cost 10 %: the channel
+// re-reads do hit L2, the slab does not; profiles/r02_scl8_nt_channel.json.)
+PCG_DEV float4 chan_ld(const float* y, uint32_t c) { return reinterpret_cast<const float4*>(y)[c]; }
 
 struct ChSt { // the channel LLRs of the lane's own codeword (stage top)
     const float* y;
