@@ -213,10 +213,12 @@ static int plan_create_impl(pcg_plan** out,
         const auto& fo = p->host.ops_fused;
         for (size_t k = 0; k < fo.size(); ++k) {
             const uint32_t c = pcg::op_code(fo[k]), st = pcg::op_stage(fo[k]) & 15u;
-            if (st == p->host.log2N - 1 && c != pcg::OP_F && c != pcg::OP_G && c != pcg::OP_G0 && c != pcg::OP_RONE &&
-                c != pcg::OP_COMB && c != pcg::OP_COPY0)
+            // the stage an op reads: its own, or its parent's (size 32) for Q16F / Q16G
+            const uint32_t rs = (c == pcg::OP_Q16F || c == pcg::OP_Q16G) ? st + 1 : st;
+            if (rs == p->host.log2N - 1 && c != pcg::OP_F && c != pcg::OP_G && c != pcg::OP_G0 &&
+                c != pcg::OP_RONE && c != pcg::OP_COMB && c != pcg::OP_COPY0)
                 v = false;
-            if (c == pcg::OP_Q16 || c == pcg::OP_Q16R)
+            if (pcg::op_has_desc(c))
                 ++k; // descriptor word
         }
         const uint32_t d = N <= 4096 ? pcg::scq_layout(N, q, v) : 0u;

@@ -152,6 +152,37 @@ void fuse_sc16(PlanHost& p)
             ++k;
         }
     }
+    // The size-32 parent's F / G folded into a fused size-16 child (the child's 16 LLRs are
+    // then computed in registers from the parent's 32): [F 5 o][Q16* 4 o][d] -> [Q16F 4 o][d'],
+    // [G 5 o][Q16* 4 o+16][d] -> [Q16G 4 o+16][d'], d' = d | (child is Q16R) << 16.
+    {
+        std::vector<uint32_t> o2;
+        for (size_t k = 0; k < out.size(); ++k) {
+            const uint32_t w = out[k], c = op_code(w);
+            if ((c == OP_F || c == OP_G) && op_stage(w) == 5 && k + 2 < out.size()) {
+                const uint32_t nx = out[k + 1], nc = op_code(nx);
+                const uint32_t oc = op_off(w) + (c == OP_G ? 16u : 0u);
+                if ((nc == OP_Q16 || nc == OP_Q16R) && op_off(nx) == oc) {
+                    o2.push_back(mkop(c == OP_F ? OP_Q16F : OP_Q16G, 16, oc));
+                    o2.push_back(out[k + 2] | (nc == OP_Q16R ? 1u << 16 : 0u));
+                    k += 2;
+                    continue;
+                }
+                // a size-16 leaf child: descriptor = leaf code | 1 << 17
+                if (nc >= OP_L_R0 && nc <= OP_L_ZSPC && nc != OP_L_DSPC8 && nc != OP_L_ZSPC8 && nc != OP_L_REPR1 &&
+                    op_stage(nx) == 4 && op_off(nx) == oc) {
+                    o2.push_back(mkop(c == OP_F ? OP_Q16F : OP_Q16G, 16, oc));
+                    o2.push_back(nc | (1u << 17));
+                    k += 1;
+                    continue;
+                }
+            }
+            o2.push_back(w);
+            if (op_has_desc(c))
+                o2.push_back(out[++k]);
+        }
+        out.swap(o2);
+    }
     // Second pass: a parent's COMB right after the last op of its right child's subtree is
     // folded into that op as a count of combine levels in the stage byte (stage | levels << 4):
     // after the op, the kernel applies COMB at stages s+1 .. s+levels going up the right
@@ -172,7 +203,7 @@ void fuse_sc16(PlanHost& p)
         p.ops_fused.push_back(w);
         end_s = s;
         end_o = o;
-        if (c == OP_Q16 || c == OP_Q16R)
+        if (op_has_desc(c))
             p.ops_fused.push_back(out[++k]); // descriptor
     }
 }

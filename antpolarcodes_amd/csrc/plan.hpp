@@ -48,6 +48,11 @@ enum OpCode : uint32_t {
     // COMB levels folded into the op (plan.cpp fuse_sc16).
     OP_Q16 = 28,
     OP_Q16R = 29,
+    // ... preceded by its parent's F (left child: OP_Q16F) or G (right child: OP_Q16G) from the
+    // size-32 stage; offset = the size-16 child's; descriptor bit 16 = the child is a Q16R,
+    // bit 17 = the child is a size-16 leaf whose code is the descriptor's low byte
+    OP_Q16F = 30,
+    OP_Q16G = 31,
     // SCL leaves (scl_avx_float.cpp)
     OP_S_R0 = 40,  // :316-337
     OP_S_R1 = 41,  // :353-413
@@ -84,6 +89,8 @@ enum StKind : uint32_t { ST_R0 = 0, ST_R1 = 1, ST_REP = 2, ST_SPC = 3, ST_RATER 
 PCG_HD inline uint32_t op_code(uint32_t w) { return w & 0xffu; }
 PCG_HD inline uint32_t op_stage(uint32_t w) { return (w >> 8) & 0xffu; }
 PCG_HD inline uint32_t op_off(uint32_t w) { return w >> 16; }
+// ops of the fused schedule followed by a descriptor word
+PCG_HD inline bool op_has_desc(uint32_t code) { return code >= 28 && code <= 31; }
 
 struct PlanHost {
     uint32_t N = 0, K = 0, L = 1, log2N = 0;

@@ -763,15 +763,133 @@ PCG_DEV uint32_t leaf8_bits(uint32_t code, const float (&x)[8])
     }
 }
 
+// A size-16 Fast-SSC leaf on 16 LLRs in registers: the 16 output sign bits.  The reference's
+// n = 16 arithmetic: AVX lane sums s_j = (+0.0 + x_j) + x_(8+j) (fastssc_avx_float.cpp:273-792).
+PCG_DEV uint32_t leaf16_bits(uint32_t code, const float (&x)[16])
+{
+    uint32_t sg = 0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+        sg |= (fbits(x[j]) >> 31) << j;
+    float s[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        s[j] = (0.0f + x[j]) + x[8 + j];
+    switch (code) {
+    case OP_L_R0:
+        return 0u;
+    case OP_L_R1:
+        return sg;
+    case OP_L_REP: { // :273-287
+        float S = s[0];
+#pragma unroll
+        for (int j = 1; j < 8; ++j)
+            S = S + s[j];
+        return (fbits(S) >> 31) ? 0xffffu : 0u;
+    }
+    case OP_L_SPC: { // :342-373: argmin lowest index, parity of all signs
+        uint32_t par = 0, m = 0;
+        float mv = __builtin_inff();
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            par ^= fbits(x[j]);
+            const float a = fabs_(x[j]);
+            if (a < mv) {
+                mv = a;
+                m = (uint32_t)j;
+            }
+        }
+        return sg ^ ((par >> 31) << m);
+    }
+    case OP_L_DREP: { // :303-332
+        const float ev = (s[0] + s[4]) + (s[2] + s[6]);
+        const float od = (s[1] + s[5]) + (s[3] + s[7]);
+        return ((fbits(ev) >> 31) ? 0x5555u : 0u) | ((fbits(od) >> 31) ? 0xaaaau : 0u);
+    }
+    case OP_L_DSPC: { // :425-466: AVX lane j's running argmin (ties -> later index), parities
+        float mv[8];
+        uint32_t mi[8];
+        uint32_t pe = 0, po = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            mv[j] = FLT_MAX_Q;
+            mi[j] = 0;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const float v = x[8 * k + j];
+                if (j & 1)
+                    po ^= fbits(v);
+                else
+                    pe ^= fbits(v);
+                const float av = fabs_(v);
+                if (!(av > mv[j])) {
+                    mv[j] = av;
+                    mi[j] = (uint32_t)(8 * k + j);
+                }
+            }
+        }
+        const float ce = minps(minps(mv[0], mv[4]), minps(mv[2], mv[6]));
+        const float co = minps(minps(mv[1], mv[5]), minps(mv[3], mv[7]));
+        uint32_t ei = 0, oi = 0;
+#pragma unroll
+        for (int j = 6; j >= 0; j -= 2)
+            if (mv[j] == ce)
+                ei = mi[j];
+#pragma unroll
+        for (int j = 7; j >= 1; j -= 2)
+            if (mv[j] == co)
+                oi = mi[j];
+        return sg ^ ((pe >> 31) << ei) ^ ((po >> 31) << oi);
+    }
+    case OP_L_TREP: { // :572-589
+        const float v[4] = { s[0] + s[4], s[1] + s[5], s[2] + s[6], s[3] + s[7] };
+        const uint32_t ob = spc4_q(v);
+        return ob | (ob << 4) | (ob << 8) | (ob << 12);
+    }
+    case OP_L_TYPE5: { // :762-792
+        float r[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            r[k] = polar_f(s[k], s[k + 4]);
+        const float R = (r[0] + r[1]) + (r[2] + r[3]);
+        float g[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            g[k] = polar_g(s[k], s[k + 4], sgn(R));
+        const uint32_t ob = spc4_q(g);
+        const uint32_t p8 = (ob ^ ((fbits(R) >> 31) ? 0xfu : 0u)) | (ob << 4);
+        return p8 | (p8 << 8);
+    }
+    case OP_L_ZSPC: { // :503-546 -- right half to both halves (Q1)
+        uint32_t par = 0, m = 0, rs = 0;
+        float mv = __builtin_inff();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const float v = x[i] + x[8 + i];
+            par ^= fbits(v);
+            rs |= (fbits(x[8 + i]) >> 31) << i;
+            const float a = fabs_(v);
+            if (a < mv) {
+                mv = a;
+                m = (uint32_t)i;
+            }
+        }
+        const uint32_t hb = rs ^ ((par >> 31) << m);
+        return hb | (hb << 8);
+    }
+    default:
+        return 0u;
+    }
+}
+
 // OP_Q16 / OP_Q16R: a size-16 node over size-8 leaves in registers on the codeword's first
 // lane -- RateRNode (:148-155: F, left leaf, G, right leaf, Combine) or ROneNode
 // (:198-219: F, left leaf, fused right rate-1).  16 LLRs in, 16 bits out.
-template <int Q, typename SRC>
-PCG_DEV void q16_body(const Cw<Q>& w, const SRC& src, uint32_t code, uint32_t o, uint32_t desc)
+// (a = the node's LLRs 0..7, b = 8..15; right = ROne node)
+template <int Q>
+PCG_DEV void q16_core(const Cw<Q>& w, const float (&a)[8], const float (&b)[8], bool rone, uint32_t o,
+                      uint32_t desc)
 {
-    const float4 c0 = src.ld(0), c1 = src.ld(1), c2 = src.ld(2), c3 = src.ld(3);
-    const float a[8] = { c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w };
-    const float b[8] = { c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w };
     float l[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -782,7 +900,7 @@ PCG_DEV void q16_body(const Cw<Q>& w, const SRC& src, uint32_t code, uint32_t o,
     for (int i = 0; i < 8; ++i)
         r[i] = polar_g(a[i], b[i], ((bl >> i) & 1u) << 31);
     uint32_t br;
-    if (code == OP_Q16) {
+    if (!rone) {
         br = leaf8_bits((desc >> 8) & 0xffu, r);
     } else { // right rate-1: bits = signs of r; left := left ^ right
         br = 0;
@@ -791,6 +909,49 @@ PCG_DEV void q16_body(const Cw<Q>& w, const SRC& src, uint32_t code, uint32_t o,
             br |= (fbits(r[i]) >> 31) << i;
     }
     w.put(o, 16, (bl ^ br) | (br << 8));
+}
+
+template <int Q, typename SRC>
+PCG_DEV void q16_body(const Cw<Q>& w, const SRC& src, uint32_t code, uint32_t o, uint32_t desc)
+{
+    const float4 c0 = src.ld(0), c1 = src.ld(1), c2 = src.ld(2), c3 = src.ld(3);
+    const float a[8] = { c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w };
+    const float b[8] = { c2.x, c2.y, c2.z, c2.w, c3.x, c3.y, c3.z, c3.w };
+    q16_core<Q>(w, a, b, code == OP_Q16R, o, desc);
+}
+
+// OP_Q16F / OP_Q16G: the size-32 parent's F (left child) or G (right child, with the
+// parent's left-half bits) from its 32 LLRs, then the child as in q16_core.
+template <int Q>
+PCG_DEV void q16x(const Cw<Q>& w, uint32_t code, uint32_t o, uint32_t desc)
+{
+    if (w.sub != 0)
+        return;
+    const bool right = code == OP_Q16G;
+    const uint32_t op = right ? o - 16u : o; // the parent's offset
+    const PSrc src = w.psrc(5);
+    float4 v[8];
+#pragma unroll
+    for (uint32_t c = 0; c < 8; ++c)
+        v[c] = src.ld(c);
+    const uint32_t lb = right ? (w.row[op >> 5] >> (op & 31u)) : 0u; // bits op .. op+15
+    float x[16];
+#pragma unroll
+    for (uint32_t i = 0; i < 16; ++i) {
+        const float p0 = q_at(v[i >> 2], i & 3u), p1 = q_at(v[4 + (i >> 2)], i & 3u);
+        x[i] = right ? polar_g(p0, p1, ((lb >> i) & 1u) << 31) : polar_f(p0, p1);
+    }
+    if ((desc >> 17) & 1u) { // the child is a size-16 leaf (code in the low byte)
+        w.put(o, 16, leaf16_bits(desc & 0xffu, x));
+        return;
+    }
+    float a[8], b[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        a[i] = x[i];
+        b[i] = x[i + 8];
+    }
+    q16_core<Q>(w, a, b, (desc >> 16) & 1u, o, desc);
 }
 
 template <int Q>
@@ -927,11 +1088,14 @@ __global__ void __launch_bounds__(64, 4) scq_kernel(KernelArgs a)
             nxt = ld_const(a.ops, k + 1 < a.nops ? k + 1 : k);
             const uint32_t code = op_code(op), s = op_stage(op) & 15u, o = op_off(op);
             const uint32_t up = op_stage(op) >> 4; // parent COMB levels folded into this op
-            if (code == OP_Q16 || code == OP_Q16R) {
+            if (op_has_desc(code)) {
                 const uint32_t desc = nxt; // the descriptor word follows
                 ++k;
                 nxt = ld_const(a.ops, k + 1 < a.nops ? k + 1 : k);
-                q16<Q>(w, code, o, desc);
+                if (code == OP_Q16F || code == OP_Q16G)
+                    q16x<Q>(w, code, o, desc);
+                else
+                    q16<Q>(w, code, o, desc);
             } else if (code >= OP_L_R0)
                 leaf_q<Q>(w, code, s, o);
             else if (code == OP_COMB || code == OP_COPY0)
@@ -996,8 +1160,8 @@ __global__ void __launch_bounds__(64, 4) scq_kernel(KernelArgs a)
         if constexpr (PROF) {
             const uint64_t t1 = __builtin_amdgcn_s_memtime();
             if (lane == 0) {
-                lprof[2 * 31] += t1 - t0; // output stage
-                lprof[2 * 31 + 1] += 1;
+                lprof[2 * 15] += t1 - t0; // output stage (slot 15: no op code)
+                lprof[2 * 15 + 1] += 1;
             }
         }
     }

@@ -26,7 +26,7 @@ torch.cuda.synchronize()
 _native.lib().pcg_dev_opprof_fetch(buf)
 names = {1: "F", 2: "G", 3: "G0", 4: "COMB", 5: "COPY0", 6: "RONE", 16: "R0", 17: "R1", 18: "REP", 19: "SPC",
          20: "DREP", 21: "DSPC", 22: "DSPC8", 23: "TREP", 24: "TYPE5", 25: "REPR1", 26: "ZSPC8", 27: "ZSPC",
-         31: "output"}
+         15: "output", 30: "Q16F", 31: "Q16G", 28: "Q16", 29: "Q16R"}
 tot = sum(buf[2 * b] for b in range(64))
 print(f"kernel {p.kernel_name()}: total {tot:.3e} wave-cycles")
 rows = []
