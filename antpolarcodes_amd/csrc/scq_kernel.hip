@@ -954,6 +954,59 @@ PCG_DEV void q16x(const Cw<Q>& w, uint32_t code, uint32_t o, uint32_t desc)
     q16_core<Q>(w, a, b, (desc >> 16) & 1u, o, desc);
 }
 
+// The fused size-16 ops across the codeword's group (Q >= 16): element i of the size-16
+// node on group lane i (the elementwise F / G in one instruction each), the size-8 leaves
+// on the eight values broadcast to every lane (the same arithmetic as q16_core / q16x, so
+// the same bits), lane 0 storing.
+template <int Q>
+PCG_DEV void q16_par(const Cw<Q>& w, uint32_t code, uint32_t o, uint32_t desc)
+{
+    const uint32_t i = w.sub & 15u;
+    const int base = (int)(__lane_id() & ~(uint32_t)(Q - 1));
+    float x;
+    if (code == OP_Q16F || code == OP_Q16G) {
+        const bool right = code == OP_Q16G;
+        const uint32_t op = right ? o - 16u : o; // the parent's offset
+        const PSrc src = w.psrc(5);
+        const float p0 = src.at(i), p1 = src.at(i + 16);
+        const uint32_t lb = right ? ((w.row[op >> 5] >> (op & 31u)) >> i) & 1u : 0u;
+        x = right ? polar_g(p0, p1, lb << 31) : polar_f(p0, p1);
+        if ((desc >> 17) & 1u) { // a size-16 leaf child
+            float xs[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                xs[j] = __shfl(x, base + j, 64);
+            const uint32_t bits = leaf16_bits(desc & 0xffu, xs);
+            if (w.sub == 0)
+                w.put(o, 16, bits);
+            return;
+        }
+    } else {
+        x = w.psrc(4).at(i);
+    }
+    const bool rone = code == OP_Q16R || ((code == OP_Q16F || code == OP_Q16G) && ((desc >> 16) & 1u));
+    const float xu = __shfl(x, base + (int)(i ^ 8u), 64); // element i + 8 on lanes i < 8
+    const float lf = polar_f(x, xu);
+    float l[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        l[j] = __shfl(lf, base + j, 64);
+    const uint32_t bl = leaf8_bits(desc & 0xffu, l);
+    const float rg = polar_g(x, xu, ((bl >> (i & 7u)) & 1u) << 31);
+    uint32_t br;
+    if (!rone) {
+        float r[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            r[j] = __shfl(rg, base + j, 64);
+        br = leaf8_bits((desc >> 8) & 0xffu, r);
+    } else { // right rate-1: the signs of r (lanes 0..7 of the group)
+        br = (uint32_t)(__ballot(sgn(rg) != 0) >> base) & 0xffu;
+    }
+    if (w.sub == 0)
+        w.put(o, 16, (bl ^ br) | (br << 8));
+}
+
 template <int Q>
 PCG_DEV void q16(const Cw<Q>& w, uint32_t code, uint32_t o, uint32_t desc)
 {
@@ -1092,7 +1145,9 @@ __global__ void __launch_bounds__(64, 4) scq_kernel(KernelArgs a)
                 const uint32_t desc = nxt; // the descriptor word follows
                 ++k;
                 nxt = ld_const(a.ops, k + 1 < a.nops ? k + 1 : k);
-                if (code == OP_Q16F || code == OP_Q16G)
+                if constexpr (Q >= 16)
+                    q16_par<Q>(w, code, o, desc);
+                else if (code == OP_Q16F || code == OP_Q16G)
                     q16x<Q>(w, code, o, desc);
                 else
                     q16<Q>(w, code, o, desc);
