@@ -21,6 +21,7 @@ struct pcg_plan {
     uint32_t wave_lds_floats = 0;
     uint32_t lds_stage_limit = 0;
     uint32_t scl_virt = 0;
+    uint32_t scl_fuse = 1;
     uint64_t scratch_floats = 0;  // per scratch unit (lane-serial wave)
     float* d_scratch = nullptr;   // grown stream-ordered (hipMallocAsync) when a launch needs more waves
     uint64_t scratch_frames = 0;  // capacity in scratch units
@@ -257,6 +258,8 @@ static int plan_create_impl(pcg_plan** out,
         p->wave_lds_floats = pcg::sc_wave_lds_floats(N);
     } else {
         rc = pcg::sclls_layout(N, L, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats, &p->scl_virt);
+        if (const char* e = getenv("PCG_SCL_FUSE"))
+            p->scl_fuse = atoi(e) != 0;
         if (rc != 0) {
             delete p;
             return fail(rc, "list decoding layout unsupported for this N/L");
@@ -544,6 +547,7 @@ static int decode_impl(pcg_plan* p,
     a.wave_lds_floats = p->wave_lds_floats;
     a.lds_stage_limit = p->lds_stage_limit;
     a.scl_virt = p->scl_virt;
+    a.scl_fuse = p->scl_fuse;
     a.scratch_floats = p->scratch_floats;
     a.fmap = fmap;
     a.fcount = fcount;

@@ -333,6 +333,85 @@ PCG_DEV void ls_fg_op(Ls<LP>& c, uint32_t s, uint32_t o, bool act)
     c.own(d);
 }
 
+// X (F or G) at stage s immediately followed by the child's F at stage s-1, with
+// alpha[s-1] in the global slab: alpha[s-1] is stored (the child's G still needs it)
+// and consumed from registers, so the F's re-read of it -- a quarter of the slab
+// traffic -- disappears.  Chunk c of alpha[s-2] needs alpha[s-1] chunks c and c+hq2,
+// i.e. alpha[s] chunks c, c+hq, c+hq2, c+hq2+hq.  s >= 5, so hq2 >= 2.
+#ifndef PCG_FGF_U
+#define PCG_FGF_U 1 // batch depth of the fused op (VGPR pressure: 2 spills 31 more registers)
+#endif
+template <int OPC, int LP, typename Src, typename Dst1, typename Dst2>
+PCG_DEV void ls_fgf(const Ls<LP>& c, Src src, Dst1 d1, Dst2 d2, uint32_t s, uint32_t o, bool act)
+{
+    constexpr int U = Pre<Src>::U >= 4 ? PCG_FGF_U : 1; // four source chunks per output chunk
+    const uint32_t hq = 1u << (s - 3), hq2 = hq >> 1;
+    const uint32_t sl = c.src_lane(s);
+    const uint32_t* row = c.row();
+    if (!act)
+        return;
+    auto load = [&](uint32_t c0, float4 (&x)[4][U]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            x[0][u] = src.ld(c0 + u, sl);
+            x[1][u] = src.ld(c0 + hq + u, sl);
+            x[2][u] = src.ld(c0 + hq2 + u, sl);
+            x[3][u] = src.ld(c0 + hq2 + hq + u, sl);
+        }
+    };
+    auto body = [&](const float4 (&x)[4][U], uint32_t c0) {
+        uint32_t wa = 0, wb = 0;
+        if (OPC == OP_G) { // 4U <= 8 elements from an 8-aligned start share a bit word
+            const uint32_t ia = o + 4u * c0, ib = ia + 4u * hq2;
+            wa = row[(ia >> 5) << 6] >> (ia & 31u);
+            wb = row[(ib >> 5) << 6] >> (ib & 31u);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float4 y0 = OPC == OP_F ? f4_f(x[0][u], x[1][u]) : f4_g(x[0][u], x[1][u], wa >> (4 * u));
+            const float4 y1 = OPC == OP_F ? f4_f(x[2][u], x[3][u]) : f4_g(x[2][u], x[3][u], wb >> (4 * u));
+            d1.st(c0 + u, y0);
+            d1.st(c0 + hq2 + u, y1);
+            d2.st(c0 + u, f4_f(y0, y1));
+        }
+    };
+    float4 xa[4][U], xb[4][U];
+    load(0, xa);
+    if (hq2 <= (uint32_t)U) {
+        body(xa, 0u);
+        return;
+    }
+    for (uint32_t c0 = 0; c0 < hq2; c0 += 2 * U) {
+        load(c0 + U, xb);
+        body(xa, c0);
+        load((c0 + 2 * U) & (hq2 - 1), xa);
+        body(xb, c0 + U);
+    }
+}
+
+template <int OPC, int LP>
+PCG_DEV void ls_fgf_op(Ls<LP>& c, uint32_t s, uint32_t o, bool act)
+{
+    const uint32_t d = s - 1, e = s - 2;
+    auto run = [&](auto dst2) {
+        const GlSt d1 = gl_st(c, d);
+        if (s == c.top)
+            ls_fgf<OPC>(c, ChSt{ c.y }, d1, dst2, s, o, act);
+        else if (s >= c.mt && o < (c.N >> 1))
+            ls_fgf<OPC>(c, RootSt<true>{ c.y, c.row(), c.N >> 3 }, d1, dst2, s, o, act);
+        else if (s >= c.mt)
+            ls_fgf<OPC>(c, RootSt<false>{ c.y, c.row(), c.N >> 3 }, d1, dst2, s, o, act);
+        else
+            ls_fgf<OPC>(c, gl_st(c, s), d1, dst2, s, o, act);
+    };
+    if (e >= c.Sl)
+        run(gl_st(c, e));
+    else
+        run(lds_st(c, e));
+    c.own(d);
+    c.own(e);
+}
+
 // Combine (avx_float.h:188-197 on packed bits): bit[o+i] ^= bit[o+h+i], i < h.
 template <int LP>
 PCG_DEV void ls_comb(const Ls<LP>& c, uint32_t s, uint32_t o, bool act)
@@ -1194,12 +1273,28 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
 #ifdef PCG_LS_PROF
             const uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
+            // an F/G whose output stage is in the global slab and whose next op is the
+            // child's F runs fused with it (ls_fgf)
+            bool fuse = false;
+            if ((code == OP_F || code == OP_G) && s >= 5 && s - 1 >= c.Sl && s - 1 < c.mt && a.scl_fuse &&
+                kop + 1 < a.nops) {
+                const uint32_t w2 = ld_const(a.ops, kop + 1);
+                fuse = op_code(w2) == OP_F && op_stage(w2) == s - 1;
+            }
             switch (code) {
             case OP_F:
-                ls_fg_op<OP_F>(c, s, o, act);
+                if (fuse) {
+                    ls_fgf_op<OP_F>(c, s, o, act);
+                    ++kop;
+                } else
+                    ls_fg_op<OP_F>(c, s, o, act);
                 break;
             case OP_G:
-                ls_fg_op<OP_G>(c, s, o, act);
+                if (fuse) {
+                    ls_fgf_op<OP_G>(c, s, o, act);
+                    ++kop;
+                } else
+                    ls_fg_op<OP_G>(c, s, o, act);
                 break;
             case OP_COMB:
                 ls_comb(c, s, o, act);
