@@ -21,7 +21,7 @@ struct pcg_plan {
     uint32_t wave_lds_floats = 0;
     uint32_t lds_stage_limit = 0;
     uint32_t scl_virt = 0;
-    uint32_t scl_fuse = 1;
+    uint32_t scl_fuse = 3;
     uint64_t scratch_floats = 0;  // per scratch unit (lane-serial wave)
     float* d_scratch = nullptr;   // grown stream-ordered (hipMallocAsync) when a launch needs more waves
     uint64_t scratch_frames = 0;  // capacity in scratch units
@@ -259,7 +259,7 @@ static int plan_create_impl(pcg_plan** out,
     } else {
         rc = pcg::sclls_layout(N, L, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats, &p->scl_virt);
         if (const char* e = getenv("PCG_SCL_FUSE"))
-            p->scl_fuse = atoi(e) != 0;
+            p->scl_fuse = (uint32_t)atoi(e);
         if (rc != 0) {
             delete p;
             return fail(rc, "list decoding layout unsupported for this N/L");

@@ -85,6 +85,7 @@ struct Ls {
     uint32_t N, L, top, Sl, mt; // mt: first recomputed stage (stages >= mt are never stored)
     LsLayout ly;
     uint32_t lane, p, gb; // lane, path index in the group, group base lane
+    uint32_t share;       // idle lanes help with F/G while P < LP (KernelArgs::scl_fuse bit 1)
     uint64_t ptr;         // slot of stage s at bits 5(s-3)
     float m;              // path metric
 #ifdef PCG_LS_PROF
@@ -258,73 +259,125 @@ PCG_DEV void stream(const Src& src, uint32_t nq, uint32_t sl, Fn&& fn)
 }
 
 // ---- F / G ---------------------------------------------------------------------------
+// Lanes working on one path's F/G.  While fewer than LP paths exist (the start of every
+// codeword: P = 1 until the first branching leaf), lanes p == path (mod P') with
+// P' = 2^ceil(log2 P) share the path's chunks instead of idling, writing into the
+// path's own column; the path's slot table and bit row are read through its lane.
+struct Share {
+    uint32_t dl;   // lane of the path worked on (its column receives the output)
+    uint32_t h, i; // lanes per path, this lane's index among them
+    bool act;
+    uint32_t sl;   // lane holding the source stage of the path
+};
+template <int LP>
+PCG_DEV Share ls_share(const Ls<LP>& c, uint32_t P, uint32_t s, uint32_t nch)
+{
+    Share w;
+    if (!c.share || 2 * P > LP || nch < 4) { // every lane on its own path (wave-uniform)
+        w.dl = c.lane;
+        w.h = 1;
+        w.i = 0;
+        w.act = c.p < P;
+        w.sl = c.src_lane(s < c.mt ? s : LS_MINS);
+        return w;
+    }
+    uint32_t pp = 1;
+    while (pp < P)
+        pp <<= 1;
+    uint32_t h = LP / pp;
+    while (h > 1 && nch < 2 * h) // at least two chunks each
+        h >>= 1;
+    const uint32_t path = c.p & (pp - 1);
+    w.dl = c.gb | path;
+    w.h = h;
+    w.i = c.p / pp;
+    w.act = path < P && w.i < h;
+    const uint32_t lo = shfl((uint32_t)c.ptr, (int)w.dl), hi = shfl((uint32_t)(c.ptr >> 32), (int)w.dl);
+    const uint64_t ptr = ((uint64_t)hi << 32) | lo;
+    w.sl = c.gb | (uint32_t)((ptr >> (5u * (s - LS_MINS))) & 31u); // stages >= mt: unused
+    return w;
+}
+template <typename S>
+struct Off { // chunks [b, ...) of a storage
+    S s;
+    uint32_t b;
+    PCG_DEV float4 ld(uint32_t c, uint32_t l) const { return s.ld(b + c, l); }
+};
+template <typename S>
+struct Pre<Off<S>> {
+    static constexpr int U = Pre<S>::U;
+};
+
 // alpha[s-1] of every active path from alpha[s] of its slot (avx_float.h:101-164),
 // h = 2^(s-1) >= 8 elements = hq float4 chunks (a power of two >= 2); the two halves
-// are streamed together.
+// are streamed together, chunks [cb, cb+n) by this lane.
 template <int OPC, int LP, typename Src, typename Dst>
-PCG_DEV void ls_fg(const Ls<LP>& c, Src src, Dst dst, uint32_t s, uint32_t o, bool act)
+PCG_DEV void ls_fg(Src src, Dst dst, const uint32_t* row, uint32_t s, uint32_t o, const Share& w)
 {
     constexpr int U = Pre<Src>::U;
-    const uint32_t hq = 1u << (s - 3);
-    const uint32_t sl = c.src_lane(s);
-    const uint32_t* row = c.row();
-    if (!act)
+    const uint32_t hq = 1u << (s - 3), n = hq / w.h, cb = n * w.i;
+    const uint32_t sl = w.sl;
+    if (!w.act)
         return;
+    const Off<Src> sa{ src, cb }, sb{ src, hq + cb };
     auto body = [&](const float4 (&xa)[U], const float4 (&xb)[U], uint32_t c0, uint32_t valid) {
         uint32_t wb = 0;
         if (OPC == OP_G) {
-            const uint32_t i = o + 4u * c0; // the batch's 4U <= 16 elements share a bit word
+            const uint32_t i = o + 4u * (cb + c0); // the batch's 4U <= 16 elements share a bit word
             wb = row[(i >> 5) << 6] >> (i & 31u);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if ((uint32_t)u < valid) {
                 const float4 r = OPC == OP_F ? f4_f(xa[u], xb[u]) : f4_g(xa[u], xb[u], wb >> (4 * u));
-                dst.st(c0 + u, r);
+                dst.st(cb + c0 + u, r);
             }
         }
     };
     float4 a0[U], b0[U], a1[U], b1[U];
-    if (hq <= 2 * U) {
-        ld_batch<U>(src, 0, hq, sl, a0);
-        ld_batch<U>(src, hq, 2 * hq, sl, b0);
-        ld_batch<U>(src, U, hq, sl, a1);
-        ld_batch<U>(src, hq + U, 2 * hq, sl, b1);
-        body(a0, b0, 0u, hq < (uint32_t)U ? hq : (uint32_t)U);
-        if (hq > (uint32_t)U)
-            body(a1, b1, (uint32_t)U, hq - U);
+    if (n <= 2 * U) {
+        ld_batch<U>(sa, 0, n, sl, a0);
+        ld_batch<U>(sb, 0, n, sl, b0);
+        ld_batch<U>(sa, U, n, sl, a1);
+        ld_batch<U>(sb, U, n, sl, b1);
+        body(a0, b0, 0u, n < (uint32_t)U ? n : (uint32_t)U);
+        if (n > (uint32_t)U)
+            body(a1, b1, (uint32_t)U, n - U);
         return;
     }
-    ld_full<U>(src, 0, sl, a0);
-    ld_full<U>(src, hq, sl, b0);
-    for (uint32_t c0 = 0; c0 < hq; c0 += 2 * U) {
-        ld_full<U>(src, c0 + U, sl, a1);
-        ld_full<U>(src, hq + c0 + U, sl, b1);
+    ld_full<U>(sa, 0, sl, a0);
+    ld_full<U>(sb, 0, sl, b0);
+    for (uint32_t c0 = 0; c0 < n; c0 += 2 * U) {
+        ld_full<U>(sa, c0 + U, sl, a1);
+        ld_full<U>(sb, c0 + U, sl, b1);
         body(a0, b0, c0, (uint32_t)U);
-        const uint32_t nx = (c0 + 2 * U) & (hq - 1);
-        ld_full<U>(src, nx, sl, a0);
-        ld_full<U>(src, hq + nx, sl, b0);
+        const uint32_t nx = (c0 + 2 * U) & (n - 1);
+        ld_full<U>(sa, nx, sl, a0);
+        ld_full<U>(sb, nx, sl, b0);
         body(a1, b1, c0 + U, (uint32_t)U);
     }
 }
 
 template <int OPC, int LP>
-PCG_DEV void ls_fg_op(Ls<LP>& c, uint32_t s, uint32_t o, bool act)
+PCG_DEV void ls_fg_op(Ls<LP>& c, uint32_t s, uint32_t o, uint32_t P)
 {
     const uint32_t d = s - 1;
     if (d >= c.mt) // recomputed where it is read
         return;
+    const Share w = ls_share(c, P, s, 1u << (s - 3));
+    const uint32_t* row = c.row_of(w.dl);
     auto run = [&](auto dst) {
+        dst.lane = w.dl;
         if (s == c.top)
-            ls_fg<OPC>(c, ChSt{ c.y }, dst, s, o, act);
+            ls_fg<OPC, LP>(ChSt{ c.y }, dst, row, s, o, w);
         else if (s >= c.mt && o < (c.N >> 1))
-            ls_fg<OPC>(c, RootSt<true>{ c.y, c.row(), c.N >> 3 }, dst, s, o, act);
+            ls_fg<OPC, LP>(RootSt<true>{ c.y, row, c.N >> 3 }, dst, row, s, o, w);
         else if (s >= c.mt)
-            ls_fg<OPC>(c, RootSt<false>{ c.y, c.row(), c.N >> 3 }, dst, s, o, act);
+            ls_fg<OPC, LP>(RootSt<false>{ c.y, row, c.N >> 3 }, dst, row, s, o, w);
         else if (s >= c.Sl)
-            ls_fg<OPC>(c, gl_st(c, s), dst, s, o, act);
+            ls_fg<OPC, LP>(gl_st(c, s), dst, row, s, o, w);
         else
-            ls_fg<OPC>(c, lds_st(c, s), dst, s, o, act);
+            ls_fg<OPC, LP>(lds_st(c, s), dst, row, s, o, w);
     };
     if (d >= c.Sl)
         run(gl_st(c, d));
@@ -342,27 +395,26 @@ PCG_DEV void ls_fg_op(Ls<LP>& c, uint32_t s, uint32_t o, bool act)
 #define PCG_FGF_U 1 // batch depth of the fused op (VGPR pressure: 2 spills 31 more registers)
 #endif
 template <int OPC, int LP, typename Src, typename Dst1, typename Dst2>
-PCG_DEV void ls_fgf(const Ls<LP>& c, Src src, Dst1 d1, Dst2 d2, uint32_t s, uint32_t o, bool act)
+PCG_DEV void ls_fgf(Src src, Dst1 d1, Dst2 d2, const uint32_t* row, uint32_t s, uint32_t o, const Share& w)
 {
     constexpr int U = Pre<Src>::U >= 4 ? PCG_FGF_U : 1; // four source chunks per output chunk
-    const uint32_t hq = 1u << (s - 3), hq2 = hq >> 1;
-    const uint32_t sl = c.src_lane(s);
-    const uint32_t* row = c.row();
-    if (!act)
+    const uint32_t hq = 1u << (s - 3), hq2 = hq >> 1, n = hq2 / w.h, cb = n * w.i;
+    const uint32_t sl = w.sl;
+    if (!w.act)
         return;
     auto load = [&](uint32_t c0, float4 (&x)[4][U]) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            x[0][u] = src.ld(c0 + u, sl);
-            x[1][u] = src.ld(c0 + hq + u, sl);
-            x[2][u] = src.ld(c0 + hq2 + u, sl);
-            x[3][u] = src.ld(c0 + hq2 + hq + u, sl);
+            x[0][u] = src.ld(cb + c0 + u, sl);
+            x[1][u] = src.ld(cb + c0 + hq + u, sl);
+            x[2][u] = src.ld(cb + c0 + hq2 + u, sl);
+            x[3][u] = src.ld(cb + c0 + hq2 + hq + u, sl);
         }
     };
     auto body = [&](const float4 (&x)[4][U], uint32_t c0) {
         uint32_t wa = 0, wb = 0;
         if (OPC == OP_G) { // 4U <= 8 elements from an 8-aligned start share a bit word
-            const uint32_t ia = o + 4u * c0, ib = ia + 4u * hq2;
+            const uint32_t ia = o + 4u * (cb + c0), ib = ia + 4u * hq2;
             wa = row[(ia >> 5) << 6] >> (ia & 31u);
             wb = row[(ib >> 5) << 6] >> (ib & 31u);
         }
@@ -370,39 +422,43 @@ PCG_DEV void ls_fgf(const Ls<LP>& c, Src src, Dst1 d1, Dst2 d2, uint32_t s, uint
         for (int u = 0; u < U; ++u) {
             const float4 y0 = OPC == OP_F ? f4_f(x[0][u], x[1][u]) : f4_g(x[0][u], x[1][u], wa >> (4 * u));
             const float4 y1 = OPC == OP_F ? f4_f(x[2][u], x[3][u]) : f4_g(x[2][u], x[3][u], wb >> (4 * u));
-            d1.st(c0 + u, y0);
-            d1.st(c0 + hq2 + u, y1);
-            d2.st(c0 + u, f4_f(y0, y1));
+            d1.st(cb + c0 + u, y0);
+            d1.st(cb + c0 + hq2 + u, y1);
+            d2.st(cb + c0 + u, f4_f(y0, y1));
         }
     };
     float4 xa[4][U], xb[4][U];
     load(0, xa);
-    if (hq2 <= (uint32_t)U) {
+    if (n <= (uint32_t)U) {
         body(xa, 0u);
         return;
     }
-    for (uint32_t c0 = 0; c0 < hq2; c0 += 2 * U) {
+    for (uint32_t c0 = 0; c0 < n; c0 += 2 * U) {
         load(c0 + U, xb);
         body(xa, c0);
-        load((c0 + 2 * U) & (hq2 - 1), xa);
+        load((c0 + 2 * U) & (n - 1), xa);
         body(xb, c0 + U);
     }
 }
 
 template <int OPC, int LP>
-PCG_DEV void ls_fgf_op(Ls<LP>& c, uint32_t s, uint32_t o, bool act)
+PCG_DEV void ls_fgf_op(Ls<LP>& c, uint32_t s, uint32_t o, uint32_t P)
 {
     const uint32_t d = s - 1, e = s - 2;
+    const Share w = ls_share(c, P, s, 1u << (s - 4));
+    const uint32_t* row = c.row_of(w.dl);
     auto run = [&](auto dst2) {
-        const GlSt d1 = gl_st(c, d);
+        GlSt d1 = gl_st(c, d);
+        d1.lane = w.dl;
+        dst2.lane = w.dl;
         if (s == c.top)
-            ls_fgf<OPC>(c, ChSt{ c.y }, d1, dst2, s, o, act);
+            ls_fgf<OPC, LP>(ChSt{ c.y }, d1, dst2, row, s, o, w);
         else if (s >= c.mt && o < (c.N >> 1))
-            ls_fgf<OPC>(c, RootSt<true>{ c.y, c.row(), c.N >> 3 }, d1, dst2, s, o, act);
+            ls_fgf<OPC, LP>(RootSt<true>{ c.y, row, c.N >> 3 }, d1, dst2, row, s, o, w);
         else if (s >= c.mt)
-            ls_fgf<OPC>(c, RootSt<false>{ c.y, c.row(), c.N >> 3 }, d1, dst2, s, o, act);
+            ls_fgf<OPC, LP>(RootSt<false>{ c.y, row, c.N >> 3 }, d1, dst2, row, s, o, w);
         else
-            ls_fgf<OPC>(c, gl_st(c, s), d1, dst2, s, o, act);
+            ls_fgf<OPC, LP>(gl_st(c, s), d1, dst2, row, s, o, w);
     };
     if (e >= c.Sl)
         run(gl_st(c, e));
@@ -1242,6 +1298,7 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
     c.mt = ls_mtop(c.top, a.scl_virt);
     c.ly = ls_layout(a.N, a.lds_stage_limit);
     c.lane = threadIdx.x;
+    c.share = (a.scl_fuse >> 1) & 1u;
     c.p = c.lane & (LP - 1);
     c.gb = c.lane & ~(uint32_t)(LP - 1);
     c.gs = a.scratch + (uint64_t)blockIdx.x * a.scratch_floats;
@@ -1276,7 +1333,7 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
             // an F/G whose output stage is in the global slab and whose next op is the
             // child's F runs fused with it (ls_fgf)
             bool fuse = false;
-            if ((code == OP_F || code == OP_G) && s >= 5 && s - 1 >= c.Sl && s - 1 < c.mt && a.scl_fuse &&
+            if ((code == OP_F || code == OP_G) && s >= 5 && s - 1 >= c.Sl && s - 1 < c.mt && (a.scl_fuse & 1u) &&
                 kop + 1 < a.nops) {
                 const uint32_t w2 = ld_const(a.ops, kop + 1);
                 fuse = op_code(w2) == OP_F && op_stage(w2) == s - 1;
@@ -1284,17 +1341,17 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
             switch (code) {
             case OP_F:
                 if (fuse) {
-                    ls_fgf_op<OP_F>(c, s, o, act);
+                    ls_fgf_op<OP_F>(c, s, o, P);
                     ++kop;
                 } else
-                    ls_fg_op<OP_F>(c, s, o, act);
+                    ls_fg_op<OP_F>(c, s, o, P);
                 break;
             case OP_G:
                 if (fuse) {
-                    ls_fgf_op<OP_G>(c, s, o, act);
+                    ls_fgf_op<OP_G>(c, s, o, P);
                     ++kop;
                 } else
-                    ls_fg_op<OP_G>(c, s, o, act);
+                    ls_fg_op<OP_G>(c, s, o, P);
                 break;
             case OP_COMB:
                 ls_comb(c, s, o, act);

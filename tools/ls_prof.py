@@ -1,30 +1,44 @@
-"""Per-op-class cycle profile of the lane-serial SCL kernel (build with -DPCG_LS_PROF;
-run with PCG_OPPROF=1).  Development aid."""
-import ctypes as C, os, sys
+"""Per-op cycle profile of sclls_kernel (development aid).  Needs a libpcg built with
+-DPCG_LS_PROF (tools/build_dev_lib.sh ls_prof -DPCG_LS_PROF) selected by PCG_DEV_LIB:
+    PCG_DEV_LIB=lib_dev/libpcg_ls_prof.so python tools/ls_prof.py [L]
+Buckets (sclls_kernel.hip, PCG_LS_PROF): op code, +8 for a global-slab source stage,
++16 for a recomputed (root child) source stage; 60 = extractBestPath + output."""
+import ctypes as C
+import os
+import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-import numpy as np
-import torch
-from antpolarcodes_amd import frames, _native
-from antpolarcodes_amd._native import Plan
-from antpolarcodes_amd.construction import frozen_bits
-N, K, L, F = 1024, 512, 8, 1 << 16
+os.environ["PCG_OPPROF"] = "1"
+import torch  # noqa: E402
+from antpolarcodes_amd import frames, _native  # noqa: E402
+from antpolarcodes_amd._native import Plan  # noqa: E402
+from antpolarcodes_amd.construction import frozen_bits  # noqa: E402
+L = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+N, K, F = 1024, 512, 1 << 16
 fz = frozen_bits(N, K, 0.0, "BB")
 llr, info, _ = frames.awgn_frames(N, fz, F, 2.0, seed=1, crc=8)
 p = Plan(N, L, fz, crc=8)
 d = torch.from_numpy(llr).cuda()
 di = torch.zeros((F, p.kb), dtype=torch.uint8, device="cuda")
 do = torch.zeros(F, dtype=torch.uint8, device="cuda")
-reps = 3
-for _ in range(reps):
-    p.decode_device(d, di, do)
-torch.cuda.synchronize()
 buf = (C.c_ulonglong * 128)()
+p.decode_device(d, di, do)
+torch.cuda.synchronize()
+_native.lib().pcg_dev_opprof_fetch(buf)  # discard the first launch
+p.decode_device(d, di, do)
+torch.cuda.synchronize()
 _native.lib().pcg_dev_opprof_fetch(buf)
-names = {1: "F lds", 2: "G lds", 9: "F gl->gl", 10: "G gl->gl", 17: "F virt", 18: "G virt", 25: "F gl->lds",
-         26: "G gl->lds", 4: "COMB", 40: "R0", 41: "R1", 43: "SPC", 44: "ST8", 60: "final", 50: "~select", 51: "~dup", 52: "~st8 move", 53: "~weak"}
-groups = buf[62]
-tot = buf[61]
-print(f"groups {groups}  cycles/group {tot / max(groups, 1):.0f}")
-for b in range(61):
+base = {1: "F", 2: "G", 4: "COMB", 40: "R0", 41: "R1", 42: "REP", 43: "SPC", 44: "ST8", 60: "output"}
+cls = {0: "", 8: " (global src)", 16: " (root child)", 24: " (?)"}
+whole = buf[61]
+print(f"kernel {p.kernel_name()}: {whole:.3e} wave-cycles over {buf[62]} codeword groups")
+rows = []
+for b in range(60):
     if buf[b]:
-        print(f"  {names.get(b, b):10s} {buf[b] / groups:10.0f} cycles/group  {100 * buf[b] / tot:5.1f}%")
+        if b < 32 and (b & 7) in (1, 2):
+            nm = base[b & 7] + cls[b & 24]
+        else:
+            nm = base.get(b, str(b))
+        rows.append((buf[b], nm))
+rows.append((buf[60], "output"))
+for cyc, nm in sorted(rows, reverse=True):
+    print(f"  {nm:20s} {100 * cyc / max(whole, 1):5.1f}%")
