@@ -836,6 +836,116 @@ PCG_DEV void grp_kmax(uint64_t& k)
     if constexpr (LP > 32) kmax_step<32>(k);
 }
 
+// ---- bitonic variant of the merge rounds (LP >= PCG_SEL_BITONIC_LP) ----------------------
+// The keys are unique, so any exact sort yields the merge rounds' order.  Lane p holds
+// elements p*K .. p*K+K-1 of the group's sequence (its locally sorted run); log2(LP)
+// bitonic merge levels double the sorted runs: a mirror stage (lane p ^ (2B-1),
+// register K-1-j) then half-cleaners (exact xor partners, then in-register pairs).
+// Every stage is K independent compare-exchanges through DPP / permlane -- no
+// dependent chain of np+1 group reductions.
+#ifndef PCG_SEL_BITONIC_LP
+#define PCG_SEL_BITONIC_LP 16
+#endif
+template <int B> // lane i <- lane i ^ (B-1) within aligned blocks of B lanes
+PCG_DEV uint32_t mirror_lane(uint32_t v)
+{
+    if constexpr (B == 2)
+        return xpartner<1>(v);
+    else if constexpr (B == 4)
+        return xpartner<2>(xpartner<1>(v)); // i ^ 3
+    else if constexpr (B == 8)
+        return bfly<4>(v); // row_half_mirror
+    else if constexpr (B == 16)
+        return bfly<8>(v); // row_mirror
+    else
+        return xpartner<16>(bfly<8>(v)); // B == 32: 31 - i
+}
+template <int B>
+PCG_DEV uint64_t mirror64(uint64_t k)
+{
+    return ((uint64_t)mirror_lane<B>((uint32_t)(k >> 32)) << 32) | mirror_lane<B>((uint32_t)k);
+}
+template <int J>
+PCG_DEV uint64_t xpart64(uint64_t k)
+{
+    return ((uint64_t)xpartner<J>((uint32_t)(k >> 32)) << 32) | xpartner<J>((uint32_t)k);
+}
+PCG_DEV uint64_t kmax(uint64_t a, uint64_t b) { return b > a ? b : a; }
+PCG_DEV uint64_t kmin(uint64_t a, uint64_t b) { return b > a ? a : b; }
+
+template <int K, int D> // half-cleaner stages at lane distances D, D/2, .., 1
+PCG_DEV void bit_lanes(uint64_t (&k)[8], uint32_t p)
+{
+    if constexpr (D >= 1) {
+        const bool low = (p & D) == 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const uint64_t o = xpart64<D>(k[j]);
+            k[j] = low ? kmax(k[j], o) : kmin(k[j], o);
+        }
+        bit_lanes<K, D / 2>(k, p);
+    }
+}
+template <int K, int D> // in-register half-cleaners at element distances D, .., 1
+PCG_DEV void bit_regs(uint64_t (&k)[8])
+{
+    if constexpr (D >= 1) {
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            if ((j & D) == 0)
+                cx_desc(k, j, j | D);
+        bit_regs<K, D / 2>(k);
+    }
+}
+template <int LP, int K, int B> // merge runs of B lanes into runs of 2B lanes
+PCG_DEV void bit_level(uint64_t (&k)[8], uint32_t p)
+{
+    if constexpr (B < LP) {
+        const bool low = (p & B) == 0;
+        uint64_t t[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            t[j] = mirror64<2 * B>(k[K - 1 - j]);
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            k[j] = low ? kmax(k[j], t[j]) : kmin(k[j], t[j]);
+        bit_lanes<K, B / 2>(k, p);
+        bit_regs<K, K / 2>(k);
+        bit_level<LP, K, 2 * B>(k, p);
+    }
+}
+
+// Float equality of two order images (+0 and -0 compare equal) in integer arithmetic
+// (a float compare here crashes this compiler's instruction selection).
+PCG_DEV bool ord_eq(uint32_t a, uint32_t b)
+{
+    const uint32_t za = a == 0x7fffffffu ? 0x80000000u : a, zb = b == 0x7fffffffu ? 0x80000000u : b;
+    return za == zb;
+}
+
+// Survivor p (< np) of the sorted group sequence and the tie test over its first R.
+template <int LP, int K>
+PCG_DEV uint64_t bit_pick(const uint64_t (&k)[8], uint32_t p, uint32_t gb, uint32_t np, uint32_t R, bool& tie)
+{
+    tie = false;
+#pragma unroll
+    for (int j = 0; j + 1 < K; ++j)
+        if (p * K + j + 1 < R)
+            tie = tie | (ord_eq((uint32_t)(k[j] >> 32), (uint32_t)(k[j + 1] >> 32)));
+    const uint32_t nxt = shfl((uint32_t)(k[0] >> 32), (int)(gb | ((p + 1) & (LP - 1))));
+    if (p + 1 < LP && p * K + K < R)
+        tie = tie | ord_eq((uint32_t)(k[K - 1] >> 32), nxt);
+    const int sl = (int)(gb | (p / K));
+    uint64_t mine = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const uint32_t lo = shfl((uint32_t)k[j], sl), hi = shfl((uint32_t)(k[j] >> 32), sl);
+        if ((uint32_t)j == p % K)
+            mine = ((uint64_t)hi << 32) | lo;
+    }
+    return p < np ? mine : 0ull;
+}
+
 template <int LP, int K>
 PCG_DEV void ls_select(const Ls<LP>& c, const float (&cv)[8], uint32_t P, uint32_t np, float& val, uint32_t& src,
                        uint32_t& jsel)
@@ -855,6 +965,10 @@ PCG_DEV void ls_select(const Ls<LP>& c, const float (&cv)[8], uint32_t P, uint32
     float prev = 0.0f;
     bool tie = false;
     uint64_t mine = 0;
+    if constexpr (LP >= PCG_SEL_BITONIC_LP) {
+        bit_level<LP, K, 1>(k, c.p);
+        mine = bit_pick<LP, K>(k, c.p, c.gb, np, R, tie);
+    } else
     for (uint32_t r = 0; r < R; ++r) {
         uint64_t h = k[0];
         grp_kmax<LP>(h);

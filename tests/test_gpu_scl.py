@@ -109,3 +109,19 @@ def test_scl32_config5_shard(oracle):
     assert np.array_equal(out[idx].cpu().numpy(), oi)
     assert np.array_equal(okh[idx].astype(np.uint8), ook)
     assert np.array_equal(met[idx].cpu().numpy().view(np.uint32), om.view(np.uint32))
+
+
+@pytest.mark.parametrize("fuse", ["0", "1", "2", "3"])
+@pytest.mark.parametrize("lds_kb", ["8", "24"])
+def test_scl_fused_and_shared_fg(oracle, monkeypatch, fuse, lds_kb):
+    """The F/G + child-F fusion (bit 0) and idle-lane sharing (bit 1) of sclls_kernel,
+    each on and off, with a small LDS budget that puts more stages in the global slab
+    (more fused pairs).  PCG_SCL_FUSE / PCG_SCL_LDS_KB are read at plan creation."""
+    from antpolarcodes_amd import frames
+    monkeypatch.setenv("PCG_SCL_FUSE", fuse)
+    monkeypatch.setenv("PCG_SCL_LDS_KB", lds_kb)
+    rng = np.random.default_rng(int(fuse) * 10 + int(lds_kb))
+    for N, L in [(256, 4), (1024, 8), (2048, 16)]:
+        fr = oracle.frozen_bits_bb(N, N // 2, 0.0)
+        llr, _, _ = frames.awgn_frames(N, fr, 48, 1.5, seed=int(rng.integers(1 << 30)), crc=8)
+        _check_scl(oracle, N, L, fr, llr)

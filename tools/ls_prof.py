@@ -1,6 +1,6 @@
 """Per-op cycle profile of sclls_kernel (development aid).  Needs a libpcg built with
 -DPCG_LS_PROF (tools/build_dev_lib.sh ls_prof -DPCG_LS_PROF) selected by PCG_DEV_LIB:
-    PCG_DEV_LIB=lib_dev/libpcg_ls_prof.so python tools/ls_prof.py [L]
+    PCG_DEV_LIB=lib_dev/libpcg_ls_prof.so python tools/ls_prof.py [L [N [F]]]
 Buckets (sclls_kernel.hip, PCG_LS_PROF): op code, +8 for a global-slab source stage,
 +16 for a recomputed (root child) source stage; 60 = extractBestPath + output."""
 import ctypes as C
@@ -13,7 +13,9 @@ from antpolarcodes_amd import frames, _native  # noqa: E402
 from antpolarcodes_amd._native import Plan  # noqa: E402
 from antpolarcodes_amd.construction import frozen_bits  # noqa: E402
 L = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-N, K, F = 1024, 512, 1 << 16
+N = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+F = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 16
+K = N // 2
 fz = frozen_bits(N, K, 0.0, "BB")
 llr, info, _ = frames.awgn_frames(N, fz, F, 2.0, seed=1, crc=8)
 p = Plan(N, L, fz, crc=8)
