@@ -1571,6 +1571,9 @@ int sclls_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* ld
     if (top > 3 + 12) // 5-bit slot fields for stages 3 .. top-1 in 64 bits
         return -4;
     uint32_t budget = 24 * 1024 / 4; // floats per wave (measured best at N = 1024, L = 8: S_l = 6, 7 waves/CU)
+    const uint32_t bitsf = 64u * (N >= 32 ? N / 32 : 1u);
+    if (bitsf + 2048u > budget) // large N: the bit rows alone fill 24 KB; keep stages 3-4 on chip
+        budget = bitsf + 2048u;  // (N = 4096: 40 KB, 4 waves/CU: +3 % over 24 KB, r02y sweep)
     if (const char* e = getenv("PCG_SCL_LDS_KB"))
         budget = (uint32_t)atoi(e) * 1024 / 4;
     uint32_t vt = ls_max_virt(top);
