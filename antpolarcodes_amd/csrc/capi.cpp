@@ -21,7 +21,7 @@ struct pcg_plan {
     uint32_t wave_lds_floats = 0;
     uint32_t lds_stage_limit = 0;
     uint32_t scl_virt = 0;
-    uint32_t scl_fuse = 3;
+    uint32_t scl_fuse = 7;
     uint64_t scratch_floats = 0;  // per scratch unit (lane-serial wave)
     float* d_scratch = nullptr;   // grown stream-ordered (hipMallocAsync) when a launch needs more waves
     uint64_t scratch_frames = 0;  // capacity in scratch units

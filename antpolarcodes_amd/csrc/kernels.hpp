@@ -28,7 +28,7 @@ struct KernelArgs {
     unsigned long long* prof; // dev-only: per-op-code [cycles, count] (null = off)
     uint32_t flags;           // dev-only experiment switches (PCG_FLAGS), 0 in production
     uint32_t scl_virt;        // lane-serial SCL: top stages recomputed instead of stored (0..2)
-    uint32_t scl_fuse;        // lane-serial SCL: bit 0 F/G + child F fused over global stages, bit 1 idle lanes share F/G (PCG_SCL_FUSE)
+    uint32_t scl_fuse;        // lane-serial SCL: bit 0 F/G + child F fused over global stages, bit 1 idle lanes share F/G, bit 2 root-child ops stage the channel in LDS (PCG_SCL_FUSE)
     // lane-serial SCL only: decode frames fmap[0 .. *fcount) (device) instead of 0 .. F-1
     // (the adaptive decoder's second stage; F bounds *fcount and sizes the grid)
     const uint32_t* fmap;

@@ -86,6 +86,7 @@ struct Ls {
     LsLayout ly;
     uint32_t lane, p, gb; // lane, path index in the group, group base lane
     uint32_t share;       // idle lanes help with F/G while P < LP (KernelArgs::scl_fuse bit 1)
+    uint32_t stage_root;  // root-child ops stage the channel in LDS (KernelArgs::scl_fuse bit 2)
     uint64_t ptr;         // slot of stage s at bits 5(s-3)
     float m;              // path metric
 #ifdef PCG_LS_PROF
@@ -441,18 +442,109 @@ PCG_DEV void ls_fgf(Src src, Dst1 d1, Dst2 d2, const uint32_t* row, uint32_t s, 
     }
 }
 
+// Fused root-child op (s = top-1: alpha[s] recomputed from the channel) with the channel
+// staged in LDS by global_load_lds.  Whenever a root child's F/G runs, the lower LDS
+// stages are dead (nothing has started yet, or the child's left subtree is finished), so
+// their region holds the channel chunks of m output chunks for every codeword of the
+// wave: one DMA instruction per 1 KB and one wait per round, instead of one dependent
+// register round trip per output chunk (these ops were ~22 % of SCL-8's cycles).
+// Staged image: codeword g, output chunk u, source k at chunk g*8m + 8u + k; k < 4 are
+// the channel chunks a_k (alpha[s] chunks c2, c2+hq, c2+hq2, c2+hq2+hq), k >= 4 the
+// chunks a_k + N/8 (their partners y_j+N/2).
+template <int OPC, bool LEFT, int LP, typename Dst2>
+PCG_DEV void ls_fgf_root(const Ls<LP>& c, GlSt d1, Dst2 d2, const uint32_t* row, uint32_t s, uint32_t o,
+                         const Share& w, uint32_t m)
+{
+    const uint32_t hq = 1u << (s - 3), hq2 = hq >> 1, hq1 = c.N >> 3;
+    float* stg = c.lds + c.ly.alpha;
+    const uint32_t per = 8u * m;                // chunks per codeword per round
+    const uint32_t ninst = (64u / LP) * per / 64u; // DMA instructions per round
+    const uint32_t n = m / w.h;                 // output chunks per lane per round
+    const uint64_t yp = (uint64_t)(uintptr_t)c.y;
+    const float4* mine = reinterpret_cast<const float4*>(stg) + (c.lane / LP) * per;
+    for (uint32_t r = 0; r < hq2; r += m) {
+        __builtin_amdgcn_s_waitcnt(0); // the previous round's LDS reads have completed
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t t = 0; t < ninst; ++t) {
+            const uint32_t f = t * 64u + c.lane;
+            const uint32_t g = f / per, rem = f % per, u = rem >> 3, k = rem & 7u;
+            uint32_t a = r + u + ((k & 1u) ? hq : 0u) + ((k & 2u) ? hq2 : 0u);
+            if (k & 4u)
+                a += hq1;
+            const uint32_t lo = shfl((uint32_t)yp, (int)(g * LP)), hi = shfl((uint32_t)(yp >> 32), (int)(g * LP));
+            const float* src = reinterpret_cast<const float*>((uintptr_t)(((uint64_t)hi << 32) | lo)) + 4u * a;
+            __builtin_amdgcn_global_load_lds(src, stg + t * 256u, 16, 0, 0);
+        }
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
+        if (!w.act)
+            continue;
+        for (uint32_t uu = 0; uu < n; ++uu) {
+            const uint32_t u = w.i * n + uu, c2 = r + u;
+            float4 yv[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                yv[k] = mine[u * 8u + k];
+            float4 x[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (LEFT) {
+                    x[k] = f4_f(yv[k], yv[k + 4]);
+                } else {
+                    const uint32_t a = c2 + ((k & 1) ? hq : 0u) + ((k & 2) ? hq2 : 0u), i = 4u * a;
+                    x[k] = f4_g(yv[k], yv[k + 4], row[(i >> 5) << 6] >> (i & 31u));
+                }
+            }
+            uint32_t wa = 0, wb = 0;
+            if (OPC == OP_G) {
+                const uint32_t ia = o + 4u * c2, ib = ia + 4u * hq2;
+                wa = row[(ia >> 5) << 6] >> (ia & 31u);
+                wb = row[(ib >> 5) << 6] >> (ib & 31u);
+            }
+            // x[1] = alpha[s] chunk c2+hq pairs with x[0]; x[2], x[3] = chunks c2+hq2, c2+hq2+hq
+            const float4 y0 = OPC == OP_F ? f4_f(x[0], x[1]) : f4_g(x[0], x[1], wa);
+            const float4 y1 = OPC == OP_F ? f4_f(x[2], x[3]) : f4_g(x[2], x[3], wb);
+            d1.st(c2, y0);
+            d1.st(c2 + hq2, y1);
+            d2.st(c2, f4_f(y0, y1));
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
+}
+
+// Output chunks per staging round of ls_fgf_root, or 0 when it does not apply: the
+// LDS stages' region must hold a round, hold no output, and give every lane a chunk.
+template <int LP>
+PCG_DEV uint32_t ls_root_round(const Ls<LP>& c, uint32_t s, uint32_t h)
+{
+    if (!c.stage_root || s != c.mt || s == c.top || s - 2 < c.Sl || c.Sl <= LS_MINS)
+        return 0;
+    const uint32_t hq2 = 1u << (s - 4);
+    const uint32_t region = 4u * 64u * ((1u << c.Sl) - 8u); // bytes
+    uint32_t m = hq2;
+    while (m > 1 && (64u / LP) * 8u * m * 16u > region)
+        m >>= 1;
+    const uint32_t need = h > LP / 8u ? h : LP / 8u;
+    return (64u / LP) * 8u * m * 16u <= region && m >= need && m >= 1 ? m : 0u;
+}
+
 template <int OPC, int LP>
 PCG_DEV void ls_fgf_op(Ls<LP>& c, uint32_t s, uint32_t o, uint32_t P)
 {
     const uint32_t d = s - 1, e = s - 2;
     const Share w = ls_share(c, P, s, 1u << (s - 4));
     const uint32_t* row = c.row_of(w.dl);
+    const uint32_t rm = ls_root_round(c, s, w.h);
     auto run = [&](auto dst2) {
         GlSt d1 = gl_st(c, d);
         d1.lane = w.dl;
         dst2.lane = w.dl;
         if (s == c.top)
             ls_fgf<OPC, LP>(ChSt{ c.y }, d1, dst2, row, s, o, w);
+        else if (rm && o < (c.N >> 1))
+            ls_fgf_root<OPC, true, LP>(c, d1, dst2, row, s, o, w, rm);
+        else if (rm)
+            ls_fgf_root<OPC, false, LP>(c, d1, dst2, row, s, o, w, rm);
         else if (s >= c.mt && o < (c.N >> 1))
             ls_fgf<OPC, LP>(RootSt<true>{ c.y, row, c.N >> 3 }, d1, dst2, row, s, o, w);
         else if (s >= c.mt)
@@ -1416,6 +1508,7 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
     c.ly = ls_layout(a.N, a.lds_stage_limit);
     c.lane = threadIdx.x;
     c.share = (a.scl_fuse >> 1) & 1u;
+    c.stage_root = (a.scl_fuse >> 2) & 1u;
     c.p = c.lane & (LP - 1);
     c.gb = c.lane & ~(uint32_t)(LP - 1);
     c.gs = a.scratch + (uint64_t)blockIdx.x * a.scratch_floats;

@@ -111,7 +111,7 @@ def test_scl32_config5_shard(oracle):
     assert np.array_equal(met[idx].cpu().numpy().view(np.uint32), om.view(np.uint32))
 
 
-@pytest.mark.parametrize("fuse", ["0", "1", "2", "3"])
+@pytest.mark.parametrize("fuse", ["0", "1", "2", "3", "5", "7"])
 @pytest.mark.parametrize("lds_kb", ["8", "24"])
 def test_scl_fused_and_shared_fg(oracle, monkeypatch, fuse, lds_kb):
     """The F/G + child-F fusion (bit 0) and idle-lane sharing (bit 1) of sclls_kernel,
