@@ -22,6 +22,7 @@ struct pcg_plan {
     uint32_t lds_stage_limit = 0;
     uint32_t scl_virt = 0;
     uint32_t scl_fuse = 7;
+    uint32_t scl_lp = 0;          // lane-serial SCL: lanes per codeword (0 = list_pow2(L))
     uint64_t scratch_floats = 0;  // per scratch unit (lane-serial wave)
     float* d_scratch = nullptr;   // grown stream-ordered (hipMallocAsync) when a launch needs more waves
     uint64_t scratch_frames = 0;  // capacity in scratch units
@@ -102,6 +103,12 @@ void free_plan_device(pcg_plan* p)
     (void)hipFree(p->d_okbuf);
 }
 
+// lanes per codeword of an adaptive plan's SCL stage, 0 = list_pow2(L).  Measured on
+// AdaptiveFloat L = 8 (profiles/r02ae_adaptive8_lp_sweep.txt): 8 lanes 6.0e7 cw/s, 16 lanes
+// 5.2e7, 32 lanes 3.3e7 -- wider groups shorten F/G but not the leaves and path selection,
+// and halve the codewords per launch round, so the list-sized group stays the default.
+constexpr uint32_t ADAPT_SCL_LP = 0;
+
 // LP: the list size rounded up to a power of two (>= 2), the lane-serial kernels' template
 uint32_t list_pow2(uint32_t L)
 {
@@ -111,7 +118,7 @@ uint32_t list_pow2(uint32_t L)
     return lp;
 }
 
-const char* kernel_name(const pcg::PlanHost& h)
+const char* kernel_name(const pcg::PlanHost& h, uint32_t scl_lp = 0)
 {
     static const char* const sclls[] = {"sclls_kernel<2>", "sclls_kernel<4>", "sclls_kernel<8>",
                                         "sclls_kernel<16>", "sclls_kernel<32>"};
@@ -123,7 +130,8 @@ const char* kernel_name(const pcg::PlanHost& h)
         return h.sc_kind == 2 ? (h.scq_q == 8 ? "scq_kernel<8>" : h.scq_q == 32 ? "scq_kernel<32>" : "scq_kernel<16>")
                               : (h.sc_kind == 0 ? "scs_kernel" : "sc_kernel");
     }
-    const int i = __builtin_ctz(list_pow2(h.L)) - 1;
+    const uint32_t lp = std::max(list_pow2(h.L), scl_lp);
+    const int i = __builtin_ctz(lp) - 1;
     return h.fixed ? sclc[i] : sclls[i];
 }
 
@@ -187,7 +195,8 @@ static int plan_create_impl(pcg_plan** out,
                             int systematic,
                             int crc_kind,
                             int device,
-                            int fixed)
+                            int fixed,
+                            uint32_t scl_lp = 0)
 {
     if (!out)
         return fail(PCG_E_ARG, "plan output pointer is null");
@@ -260,12 +269,19 @@ static int plan_create_impl(pcg_plan** out,
         rc = pcg::sclls_layout(N, L, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats, &p->scl_virt);
         if (const char* e = getenv("PCG_SCL_FUSE"))
             p->scl_fuse = (uint32_t)atoi(e);
+        // lanes per codeword: the caller's request or the PCG_SCL_LP dev override, used when
+        // it is a power of two between list_pow2(L) and 32
+        if (const char* e = getenv("PCG_SCL_LP"))
+            scl_lp = (uint32_t)strtoul(e, nullptr, 10);
+        p->scl_lp = list_pow2(L);
+        if (scl_lp > p->scl_lp && scl_lp <= 32 && (scl_lp & (scl_lp - 1)) == 0)
+            p->scl_lp = scl_lp;
         if (rc != 0) {
             delete p;
             return fail(rc, "list decoding layout unsupported for this N/L");
         }
     }
-    p->kernel = kernel_name(p->host);
+    p->kernel = kernel_name(p->host, p->scl_lp);
     p->dev_opprof = getenv("PCG_OPPROF") != nullptr;
     if (const char* fl = getenv("PCG_FLAGS"))
         p->dev_flags = (uint32_t)strtoul(fl, nullptr, 0);
@@ -311,7 +327,7 @@ static int plan_create_impl(pcg_plan** out,
     } else if (!h.fixed && h.L == 1 && h.sc_kind == 0) {
         p->wave_cap = pcg::scs_wave_cap(p->wave_lds_floats);
     } else if (!h.fixed && h.L > 1) {
-        p->wave_cap = pcg::sclls_wave_cap(h.L, p->wave_lds_floats);
+        p->wave_cap = pcg::sclls_wave_cap(p->scl_lp, p->wave_lds_floats);
         const char* q = getenv("PCG_SCL_QUEUE"); // dev switch: 0 = static grid stride
         if (!(q && q[0] == '0')) {
             if ((e = hipMalloc(&p->d_queue, 2 * sizeof(uint32_t))) != hipSuccess ||
@@ -377,7 +393,13 @@ static int plan_create_adaptive_impl(pcg_plan** out,
 {
     if (L < 2) // makeDecoder with listSize 1 builds the plain Fast-SSC decoder (decoder.cpp:60-68)
         return plan_create_impl(out, N, L, frozen, n_frozen, systematic, crc_kind, device, fixed);
-    int rc = plan_create_impl(out, N, L, frozen, n_frozen, systematic, crc_kind, device, fixed);
+    // The SCL stage decodes only the Fast-SSC failures: a few frames per launch at useful
+    // SNRs, so its time is about one walk's latency.  PCG_ADAPT_LP (dev override) runs it
+    // with wider lane groups, the lanes beyond the list sharing every F/G.
+    uint32_t lp = ADAPT_SCL_LP;
+    if (const char* e = getenv("PCG_ADAPT_LP"))
+        lp = (uint32_t)strtoul(e, nullptr, 10);
+    int rc = plan_create_impl(out, N, L, frozen, n_frozen, systematic, crc_kind, device, fixed, fixed ? 0 : lp);
     if (rc != 0)
         return rc;
     pcg_plan* fast = nullptr;
@@ -594,7 +616,8 @@ static int decode_impl(pcg_plan* p,
     } else if (h.L == 1) {
         rc = pcg::launch_sc(a, s);
     } else {
-        a.units = (uint32_t)pcg::wave_units(F, 64 / list_pow2(h.L), p->wave_cap);
+        a.scl_lp = p->scl_lp;
+        a.units = (uint32_t)pcg::wave_units(F, 64 / p->scl_lp, p->wave_cap);
         if ((rc = grow_scratch(p, a.units, sizeof(float), s)) != 0)
             return rc;
         a.scratch = p->d_scratch;

@@ -49,6 +49,10 @@ struct KernelArgs {
     float metric0;
     // Fast-SSC (sc_kernel.hip): F x N soft codeword output (Decoder::getSoftCodeword) or null
     float* soft;
+    // lane-serial SCL: lanes per codeword (a power of two >= the list size rounded up; 0 =
+    // that minimum).  Wider groups give the idle lanes F/G work (ls_share): the adaptive
+    // decoder's second stage, a few frames at a time, runs latency-bound walks.
+    uint32_t scl_lp;
 };
 
 // PCG_*_WPC developer overrides of the waves per CU: ignored unless a positive number
@@ -106,7 +110,7 @@ inline uint64_t wave_units(uint64_t F, uint32_t frames_per_wave, uint64_t cap)
 // lane-serial SCL kernel (sclls_kernel.hip), 64 / L' codewords per wave
 int sclls_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* lds_stage_limit,
                  uint64_t* scratch_floats, uint32_t* virt);
-uint64_t sclls_wave_cap(uint32_t L, uint32_t wave_lds_floats);
+uint64_t sclls_wave_cap(uint32_t lp, uint32_t wave_lds_floats);
 int launch_sclls(const KernelArgs& a, hipStream_t stream);
 // 8-bit SCL (scl_char_kernel.hip): LDS dwords per wave, LDS stage limit, global scratch dwords
 int sclc_layout(uint32_t N, uint32_t L, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratch_dwords);

@@ -529,8 +529,8 @@ int launch_sccs(const KernelArgs& a, hipStream_t stream)
 {
     const bool i8 = a.llr8 != nullptr;
     const uint64_t grid = a.units;
-    if (grid == 0)
-        return 0;
+    if (grid == 0) // no waves for a non-empty batch: an error, never a silent no-op
+        return a.F ? -4 : 0;
     const size_t lds = (size_t)a.wave_lds_floats * 4u;
     if (i8)
         hipLaunchKernelGGL((sccs_kernel<true>), dim3((uint32_t)grid), dim3(64), lds, stream, a, a.lds_stage_limit);

@@ -1715,14 +1715,14 @@ static int ls_resident(uint32_t lds_bytes)
 
 // Waves (= scratch units) for a launch of F frames: one persistent wave per resident
 // slot (hipOccupancy: VGPR / LDS limits), capped at PCG_SCL_WPC waves per CU.
-uint64_t sclls_wave_cap(uint32_t L, uint32_t wave_lds_floats)
+uint64_t sclls_wave_cap(uint32_t lp, uint32_t wave_lds_floats)
 {
     int dev = 0, cus = 256;
     if (hipGetDevice(&dev) == hipSuccess)
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const uint32_t lds = wave_lds_floats * 4u;
     int res = 0;
-    switch (lp_of(L)) {
+    switch (lp) {
     case 2: res = ls_resident<2>(lds); break;
     case 4: res = ls_resident<4>(lds); break;
     case 8: res = ls_resident<8>(lds); break;
@@ -1742,13 +1742,14 @@ uint64_t sclls_wave_cap(uint32_t L, uint32_t wave_lds_floats)
 int launch_sclls(const KernelArgs& a, hipStream_t stream)
 {
     const uint64_t grid = a.units;
-    if (grid == 0)
-        return 0;
+    if (grid == 0) // no waves for a non-empty batch: an error, never a silent no-op
+        return a.F ? -4 : 0;
     size_t lds = (size_t)a.wave_lds_floats * sizeof(float);
 #ifdef PCG_LS_PROF
     lds += 64 * sizeof(uint64_t);
 #endif
-    switch (lp_of(a.L)) {
+    const uint32_t lp = a.scl_lp > lp_of(a.L) ? a.scl_lp : lp_of(a.L);
+    switch (lp) {
     case 2: hipLaunchKernelGGL(sclls_kernel<2>, dim3((uint32_t)grid), dim3(64), lds, stream, a); break;
     case 4: hipLaunchKernelGGL(sclls_kernel<4>, dim3((uint32_t)grid), dim3(64), lds, stream, a); break;
     case 8: hipLaunchKernelGGL(sclls_kernel<8>, dim3((uint32_t)grid), dim3(64), lds, stream, a); break;

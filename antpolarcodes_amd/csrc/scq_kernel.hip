@@ -1274,8 +1274,8 @@ uint64_t scq_wave_cap(uint32_t Q, bool V, uint32_t lds_dwords)
 int launch_scq(const KernelArgs& a, uint32_t Q, bool V, hipStream_t stream)
 {
     const uint64_t grid = a.units;
-    if (grid == 0)
-        return 0;
+    if (grid == 0) // no waves for a non-empty batch: an error, never a silent no-op
+        return a.F ? -4 : 0;
     const size_t lds = (size_t)a.wave_lds_floats * 4u + (a.prof ? 128 * sizeof(unsigned long long) : 0);
 #define PCG_SCQ_LAUNCH(QV, VV)                                                                              \
     if (a.prof)                                                                                             \

@@ -673,8 +673,8 @@ uint64_t scs_wave_cap(uint32_t lds_dwords)
 int launch_scs(const KernelArgs& a, hipStream_t stream)
 {
     const uint64_t grid = a.units;
-    if (grid == 0)
-        return 0;
+    if (grid == 0) // no waves for a non-empty batch: an error, never a silent no-op
+        return a.F ? -4 : 0;
     hipLaunchKernelGGL(scs_kernel, dim3((uint32_t)grid), dim3(64), (size_t)a.wave_lds_floats * 4u, stream, a,
                        a.lds_stage_limit);
     return hipGetLastError() == hipSuccess ? 0 : -3;

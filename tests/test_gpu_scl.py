@@ -125,3 +125,23 @@ def test_scl_fused_and_shared_fg(oracle, monkeypatch, fuse, lds_kb):
         fr = oracle.frozen_bits_bb(N, N // 2, 0.0)
         llr, _, _ = frames.awgn_frames(N, fr, 48, 1.5, seed=int(rng.integers(1 << 30)), crc=8)
         _check_scl(oracle, N, L, fr, llr)
+
+
+@pytest.mark.parametrize("lp", ["16", "32"])
+@pytest.mark.parametrize("fuse", ["3", "7"])
+def test_scl_wide_lane_groups(oracle, monkeypatch, lp, fuse):
+    """Lists decoded in lane groups wider than the list (PCG_SCL_LP; the adaptive
+    decoder's SCL stage runs this way): the lanes beyond the list share every F/G.
+    Bit-exact vs the oracle over the tie-heavy LLR families and AWGN frames."""
+    from antpolarcodes_amd import frames
+    monkeypatch.setenv("PCG_SCL_LP", lp)
+    monkeypatch.setenv("PCG_SCL_FUSE", fuse)
+    rng = np.random.default_rng(int(lp) + int(fuse))
+    for N, L in [(64, 2), (256, 4), (1024, 8), (1024, 16)]:
+        if L >= int(lp):
+            continue
+        fr = oracle.frozen_bits_bb(N, N // 2, 0.0)
+        llr, _, _ = frames.awgn_frames(N, fr, 64, 1.0, seed=int(rng.integers(1 << 30)), crc=8)
+        _check_scl(oracle, N, L, fr, llr)
+        for kind in LLR_KINDS:
+            _check_scl(oracle, N, L, fr, llr_kinds(rng, 8, N, kind))
