@@ -38,6 +38,8 @@ class PlanDesc(C.Structure):
         ("scratch_bytes", C.c_uint64),
         ("crc_kind", C.c_int32),
         ("systematic", C.c_int32),
+        ("lanes_per_codeword", C.c_uint32),
+        ("dev_overrides", C.c_uint32),  # PCG_DEV_* bits: non-default kernel/layout from dev env switches
     ]
 
 

@@ -30,7 +30,7 @@ struct pcg_plan {
     // evaluated once at plan creation
     uint64_t wave_cap = 0;
     uint64_t wave_cap_i8 = 0;
-    uint32_t* d_queue = nullptr;  // lane-serial SCL work queue: two zeroed counters
+    uint32_t* d_queue = nullptr;  // lane-serial SCL work queue: one counter, zeroed on the launch stream
     const char* kernel = "";      // name of the decode kernel (pcg_plan_kernel_name)
     // developer switches, read from the environment once at plan creation
     uint32_t dev_flags = 0;
@@ -51,6 +51,17 @@ struct pcg_plan {
     uint32_t* d_fmap = nullptr;
     uint8_t* d_okbuf = nullptr;
     uint64_t fmap_frames = 0;
+    // pcg_decode_f32_soft_host staging (the float staging above holds the LLRs)
+    float* d_soft = nullptr;
+    uint64_t soft_frames = 0;
+    // Stream ordering of the plan's buffers (scratch, queue, staging, frame map): the
+    // event is recorded after every decode on the stream it ran on, and a decode on a
+    // different stream first waits for it, so launches of one plan never overlap whatever
+    // streams callers use; pcg_plan_destroy waits for it before freeing.
+    hipEvent_t last_ev = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool has_last = false;
+    uint32_t dev_overrides = 0;   // PCG_DEV_* bits: developer switches that changed this plan
 };
 
 namespace {
@@ -86,13 +97,21 @@ struct DeviceGuard {
 
 void free_plan_device(pcg_plan* p)
 {
+    // everything queued on the plan's buffers has finished once its last event has
+    if (p->has_last)
+        (void)hipEventSynchronize(p->last_ev);
     (void)hipFree(p->d_ops);
     (void)hipFree(p->d_info_pos);
     (void)hipFree(p->d_crc_m);
-    if (p->d_scratch) { // stream-ordered allocation: free it in order, then wait
+    if (p->d_scratch) { // stream-ordered allocation (idle now): return it to the pool
         (void)hipFreeAsync(p->d_scratch, nullptr);
         (void)hipStreamSynchronize(nullptr);
     }
+    (void)hipFree(p->d_soft);
+    if (p->last_ev)
+        (void)hipEventDestroy(p->last_ev);
+    p->last_ev = nullptr;
+    p->has_last = false;
     (void)hipFree(p->d_queue);
     (void)hipFree(p->d_llr);
     (void)hipFree(p->d_info);
@@ -150,6 +169,30 @@ int grow_scratch(pcg_plan* p, uint64_t units, size_t elem, hipStream_t s)
         return hip_fail(e, "hipMallocAsync(scratch)");
     p->d_scratch = static_cast<float*>(ptr);
     p->scratch_frames = units;
+    return PCG_OK;
+}
+
+// Order a decode on `s` after the plan's previous decode (on whatever stream that ran).
+int order_on(pcg_plan* p, hipStream_t s)
+{
+    if (p->has_last && p->last_stream != s) {
+        hipError_t e = hipStreamWaitEvent(s, p->last_ev, 0);
+        if (e != hipSuccess)
+            return hip_fail(e, "hipStreamWaitEvent(plan order)");
+    }
+    return PCG_OK;
+}
+
+// Record the end of a decode on `s`.
+int mark_done(pcg_plan* p, hipStream_t s)
+{
+    if (!p->last_ev)
+        return PCG_OK;
+    hipError_t e = hipEventRecord(p->last_ev, s);
+    if (e != hipSuccess)
+        return hip_fail(e, "hipEventRecord(plan order)");
+    p->last_stream = s;
+    p->has_last = true;
     return PCG_OK;
 }
 
@@ -214,11 +257,15 @@ static int plan_create_impl(pcg_plan** out,
         // LDS-resident Fast-SSC: Q lanes per codeword (PCG_SCQ_Q dev override), while a
         // wave's state fits a CU and leaves room for several waves
         uint32_t q = 16;
-        if (const char* e = getenv("PCG_SCQ_Q"))
+        if (const char* e = getenv("PCG_SCQ_Q")) {
             q = (uint32_t)atoi(e);
+            p->dev_overrides |= PCG_DEV_SCQ;
+        }
         bool v = true; // the root's children recomputed from the channel (half the LDS)
-        if (const char* e = getenv("PCG_SCQ_VIRT"))
+        if (const char* e = getenv("PCG_SCQ_VIRT")) {
             v = e[0] != '0';
+            p->dev_overrides |= PCG_DEV_SCQ;
+        }
         // ... only F / G / G0 / ROne read them (leaves and fused size-16 ops read stored stages)
         const auto& fo = p->host.ops_fused;
         for (size_t k = 0; k < fo.size(); ++k) {
@@ -267,12 +314,16 @@ static int plan_create_impl(pcg_plan** out,
         p->wave_lds_floats = pcg::sc_wave_lds_floats(N);
     } else {
         rc = pcg::sclls_layout(N, L, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats, &p->scl_virt);
-        if (const char* e = getenv("PCG_SCL_FUSE"))
+        if (const char* e = getenv("PCG_SCL_FUSE")) {
             p->scl_fuse = (uint32_t)atoi(e);
-        // lanes per codeword: the caller's request or the PCG_SCL_LP dev override, used when
-        // it is a power of two between list_pow2(L) and 32
-        if (const char* e = getenv("PCG_SCL_LP"))
+            p->dev_overrides |= PCG_DEV_SCL_FUSE;
+        }
+        // lanes per codeword: the caller's request, else the PCG_SCL_LP dev override; used
+        // when it is a power of two between list_pow2(L) and 32
+        if (const char* e = getenv("PCG_SCL_LP"); e && scl_lp == 0) {
             scl_lp = (uint32_t)strtoul(e, nullptr, 10);
+            p->dev_overrides |= PCG_DEV_SCL_LP;
+        }
         p->scl_lp = list_pow2(L);
         if (scl_lp > p->scl_lp && scl_lp <= 32 && (scl_lp & (scl_lp - 1)) == 0)
             p->scl_lp = scl_lp;
@@ -283,8 +334,19 @@ static int plan_create_impl(pcg_plan** out,
     }
     p->kernel = kernel_name(p->host, p->scl_lp);
     p->dev_opprof = getenv("PCG_OPPROF") != nullptr;
-    if (const char* fl = getenv("PCG_FLAGS"))
+    if (p->dev_opprof)
+        p->dev_overrides |= PCG_DEV_OPPROF;
+    if (const char* fl = getenv("PCG_FLAGS")) {
         p->dev_flags = (uint32_t)strtoul(fl, nullptr, 0);
+        if (p->dev_flags)
+            p->dev_overrides |= PCG_DEV_FLAGS;
+    }
+    for (const char* v : {"PCG_SC_KERNEL", "PCG_SCL_LDS_KB", "PCG_SCL_STAGE_LIMIT", "PCG_SCL_VIRT", "PCG_SCL_QUEUE",
+                          "PCG_SCQ_WPC", "PCG_SCS_WPC", "PCG_SCL_WPC", "PCG_SCCS_WPC", "PCG_SCLC_WPC",
+                          "PCG_SCS_LDS_KB", "PCG_SCS_SL", "PCG_SCCS_LDS_KB", "PCG_SCCS_SL", "PCG_SCLC_LDS_KB",
+                          "PCG_SCLC_SL"})
+        if (getenv(v))
+            p->dev_overrides |= PCG_DEV_LAYOUT;
     if (device < 0) { // host-only plan: classification / validation without a GPU
         p->device = -1;
         *out = p;
@@ -307,6 +369,11 @@ static int plan_create_impl(pcg_plan** out,
     }
     const auto& h = p->host;
     hipError_t e;
+    if ((e = hipEventCreateWithFlags(&p->last_ev, hipEventDisableTiming)) != hipSuccess) {
+        p->last_ev = nullptr;
+        delete p;
+        return hip_fail(e, "hipEventCreate(plan order)");
+    }
     if ((e = hipMalloc(&p->d_ops, 4 * std::max<size_t>(1, h.ops.size() + h.ops_fused.size()))) != hipSuccess ||
         // info positions padded to whole 16-byte groups (scq_kernel.hip reads 8 at once)
         (e = hipMalloc(&p->d_info_pos, 2 * (h.info_pos.size() + 16))) != hipSuccess ||
@@ -330,8 +397,7 @@ static int plan_create_impl(pcg_plan** out,
         p->wave_cap = pcg::sclls_wave_cap(p->scl_lp, p->wave_lds_floats);
         const char* q = getenv("PCG_SCL_QUEUE"); // dev switch: 0 = static grid stride
         if (!(q && q[0] == '0')) {
-            if ((e = hipMalloc(&p->d_queue, 2 * sizeof(uint32_t))) != hipSuccess ||
-                (e = hipMemset(p->d_queue, 0, 2 * sizeof(uint32_t))) != hipSuccess) {
+            if ((e = hipMalloc(&p->d_queue, sizeof(uint32_t))) != hipSuccess) {
                 free_plan_device(p);
                 delete p;
                 return hip_fail(e, "hipMalloc(work queue)");
@@ -397,11 +463,14 @@ static int plan_create_adaptive_impl(pcg_plan** out,
     // SNRs, so its time is about one walk's latency.  PCG_ADAPT_LP (dev override) runs it
     // with wider lane groups, the lanes beyond the list sharing every F/G.
     uint32_t lp = ADAPT_SCL_LP;
-    if (const char* e = getenv("PCG_ADAPT_LP"))
-        lp = (uint32_t)strtoul(e, nullptr, 10);
+    const char* lpe = getenv("PCG_ADAPT_LP");
+    if (lpe)
+        lp = (uint32_t)strtoul(lpe, nullptr, 10);
     int rc = plan_create_impl(out, N, L, frozen, n_frozen, systematic, crc_kind, device, fixed, fixed ? 0 : lp);
     if (rc != 0)
         return rc;
+    if (lpe)
+        (*out)->dev_overrides |= PCG_DEV_SCL_LP;
     pcg_plan* fast = nullptr;
     // the Fast-SSC stage rejects what its constructor rejects (invalid_argument)
     rc = plan_create_impl(&fast, N, 1, frozen, n_frozen, systematic, crc_kind, device, fixed);
@@ -467,6 +536,9 @@ int pcg_plan_describe(const pcg_plan* p, pcg_plan_desc* d)
     d->scratch_bytes = p->scratch_floats * 4;
     d->crc_kind = p->host.crc_kind;
     d->systematic = p->host.systematic;
+    d->lanes_per_codeword = p->host.L > 1 && !p->host.fixed ? p->scl_lp
+                          : (p->host.L == 1 && p->host.sc_kind == 2 ? p->host.scq_q : 0);
+    d->dev_overrides = p->dev_overrides | (p->fast ? p->fast->dev_overrides : 0u);
     return PCG_OK;
 }
 
@@ -489,6 +561,9 @@ static int decode_adaptive(pcg_plan* p, const float* llr, uint64_t F, uint8_t* i
     // for the frames whose check failed, whose SCL output (and ok) replaces the SC one.
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     hipError_t e;
+    int rc = order_on(p, s); // d_fmap / d_okbuf are reused: after the previous call's readers
+    if (rc != 0)
+        return rc;
     if (p->fmap_frames < F) {
         (void)hipFree(p->d_fmap);
         (void)hipFree(p->d_okbuf);
@@ -500,7 +575,7 @@ static int decode_adaptive(pcg_plan* p, const float* llr, uint64_t F, uint8_t* i
         p->fmap_frames = F;
     }
     uint8_t* okb = ok ? ok : p->d_okbuf;
-    int rc = decode_impl(p->fast, llr, F, info, okb, nullptr, stream, nullptr, nullptr, llr8);
+    rc = decode_impl(p->fast, llr, F, info, okb, nullptr, stream, nullptr, nullptr, llr8);
     if (rc != 0)
         return rc;
     if (metrics && (e = hipMemsetAsync(metrics, 0, F * p->host.L * sizeof(float), s)) != hipSuccess)
@@ -583,7 +658,9 @@ static int decode_impl(pcg_plan* p,
     a.flags = p->dev_flags;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const bool i8 = llr8 != nullptr;
-    int rc;
+    int rc = order_on(p, s);
+    if (rc != 0)
+        return rc;
     if (soft) { // soft codeword: the one-codeword-per-wave Fast-SSC kernel (float plans, L = 1)
         a.soft = soft;
         a.wave_lds_floats = pcg::sc_wave_lds_floats(h.N);
@@ -622,11 +699,16 @@ static int decode_impl(pcg_plan* p,
             return rc;
         a.scratch = p->d_scratch;
         a.queue = p->d_queue;
+        if (a.queue) { // the work-queue counter starts at 0 for every launch, in stream order
+            hipError_t e = hipMemsetAsync(a.queue, 0, sizeof(uint32_t), s);
+            if (e != hipSuccess)
+                return hip_fail(e, "hipMemsetAsync(work queue)");
+        }
         rc = pcg::launch_sclls(a, s);
     }
     if (rc != 0)
         return fail(rc, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
-    return PCG_OK;
+    return mark_done(p, s);
 }
 
 int pcg_decode_i8(pcg_plan* p,
@@ -808,29 +890,45 @@ int pcg_decode_f32_soft_host(pcg_plan* p, const float* llr, uint64_t F, uint8_t*
         return fail(PCG_E_NODEVICE, "host-only plan (created with device < 0)");
     DeviceGuard g(p->device);
     const uint64_t N = p->host.N, kb = (p->host.K + 7) / 8;
-    float* d_llr = nullptr;
-    float* d_soft = nullptr;
-    uint8_t* d_info = nullptr;
-    uint8_t* d_ok = nullptr;
     hipError_t e;
-    if ((e = hipMalloc(&d_llr, F * N * sizeof(float))) != hipSuccess ||
-        (e = hipMalloc(&d_soft, F * N * sizeof(float))) != hipSuccess ||
-        (e = hipMalloc(&d_info, F * std::max<uint64_t>(kb, 1))) != hipSuccess ||
-        (e = hipMalloc(&d_ok, F)) != hipSuccess) {
-        rc = hip_fail(e, "hipMalloc(soft staging)");
-    } else if ((e = hipMemcpy(d_llr, llr, F * N * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess) {
-        rc = hip_fail(e, "hipMemcpy(H2D)");
-    } else if ((rc = pcg_decode_f32_soft(p, d_llr, F, d_info, d_ok, d_soft, nullptr)) == 0) {
-        if ((e = hipMemcpy(info, d_info, F * kb, hipMemcpyDeviceToHost)) != hipSuccess ||
-            (e = hipMemcpy(soft, d_soft, F * N * sizeof(float), hipMemcpyDeviceToHost)) != hipSuccess ||
-            (ok && (e = hipMemcpy(ok, d_ok, F, hipMemcpyDeviceToHost)) != hipSuccess))
-            rc = hip_fail(e, "hipMemcpy(D2H)");
+    // staging kept in the plan (pcg_decode_f32_host's buffers + a soft-codeword buffer);
+    // the null-stream copies below are ordered after the plan's previous decode
+    if ((rc = order_on(p, nullptr)) != 0)
+        return rc;
+    if (p->stage_frames < F || p->soft_frames < F) {
+        if ((e = hipStreamSynchronize(nullptr)) != hipSuccess)
+            return hip_fail(e, "hipStreamSynchronize");
+        const uint64_t n = std::max(F, p->stage_frames);
+        (void)hipFree(p->d_llr);
+        (void)hipFree(p->d_info);
+        (void)hipFree(p->d_ok);
+        (void)hipFree(p->d_met);
+        (void)hipFree(p->d_soft);
+        p->d_llr = nullptr;
+        p->d_info = nullptr;
+        p->d_ok = nullptr;
+        p->d_met = nullptr;
+        p->d_soft = nullptr;
+        p->stage_frames = 0;
+        p->soft_frames = 0;
+        if ((e = hipMalloc(&p->d_llr, n * N * sizeof(float))) != hipSuccess ||
+            (e = hipMalloc(&p->d_info, n * std::max<uint64_t>(kb, 1))) != hipSuccess ||
+            (e = hipMalloc(&p->d_ok, n)) != hipSuccess ||
+            (e = hipMalloc(&p->d_met, n * p->host.L * sizeof(float))) != hipSuccess ||
+            (e = hipMalloc(&p->d_soft, n * N * sizeof(float))) != hipSuccess)
+            return hip_fail(e, "hipMalloc(soft staging)");
+        p->stage_frames = n;
+        p->soft_frames = n;
     }
-    (void)hipFree(d_llr);
-    (void)hipFree(d_soft);
-    (void)hipFree(d_info);
-    (void)hipFree(d_ok);
-    return rc;
+    if ((e = hipMemcpy(p->d_llr, llr, F * N * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
+        return hip_fail(e, "hipMemcpy(H2D)");
+    if ((rc = pcg_decode_f32_soft(p, p->d_llr, F, p->d_info, p->d_ok, p->d_soft, nullptr)) != 0)
+        return rc;
+    if ((e = hipMemcpy(info, p->d_info, F * kb, hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemcpy(soft, p->d_soft, F * N * sizeof(float), hipMemcpyDeviceToHost)) != hipSuccess ||
+        (ok && (e = hipMemcpy(ok, p->d_ok, F, hipMemcpyDeviceToHost)) != hipSuccess))
+        return hip_fail(e, "hipMemcpy(D2H)");
+    return PCG_OK;
 }
 
 int pcg_decode_punctured_f32(pcg_plan* p,
@@ -857,6 +955,9 @@ int pcg_decode_punctured_f32(pcg_plan* p,
     DeviceGuard g(p->device);
     const auto& h = p->host;
     const uint64_t kb = (h.K + 7) / 8;
+    // d_dep is reused: the depuncture below runs after the plan's previous decode
+    if (int rc = order_on(p, reinterpret_cast<hipStream_t>(stream)); rc != 0)
+        return rc;
     // depunctured staging: at most 256 MB per chunk
     const uint64_t chunk = std::min<uint64_t>(F, std::max<uint64_t>(1, (1ull << 26) / h.N));
     if (p->dep_frames < chunk) {

@@ -3,6 +3,7 @@
 // top of the C ABI (include/pcg.h).  No device code here.
 #include <polarcode/construction/constructor.h>
 #include <polarcode/decoding/decoder.h>
+#include <polarcode/encoding/butterfly_fip_packed.h>
 #include <polarcode/encoding/encoder.h>
 #include <polarcode/errordetection/errordetector.h>
 #include <polarcode/puncturer.h>
@@ -13,6 +14,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <stdexcept>
 
@@ -268,56 +270,123 @@ void Puncturer::puncturePacked(unsigned char* pOutput, const unsigned char* pInp
 // =============================================================== Encoding
 namespace Encoding {
 
-Encoder::Encoder() : mErrorDetector(&ErrorDetection::globalDummyDetector), mBlockLength(0), mSystematic(true) {}
+Encoder::Encoder()
+    : mEncoderDuration(0), mErrorDetector(&ErrorDetection::globalDummyDetector), mBlockLength(0), mSystematic(true),
+      mCodewordReady(false), xmInputData(nullptr), mBitContainer(nullptr)
+{
+}
+
+Encoder::~Encoder() { delete mBitContainer; }
+
+size_t Encoder::blockLength() { return mBlockLength; }
+
+void Encoder::setErrorDetection(ErrorDetection::Detector* pDetector) { mErrorDetector = pDetector; }
+
+void Encoder::setSystematic(bool sys) { mSystematic = sys; }
+
+bool Encoder::isSystematic() { return mSystematic; }
+
+void Encoder::setInformation(void* pData) { xmInputData = static_cast<unsigned char*>(pData); }
+
+void Encoder::getInformation(void* pData) { mBitContainer->getPackedInformationBits(pData); }
+
+void Encoder::setCodeword(void* pData)
+{
+    xmInputData = static_cast<unsigned char*>(pData);
+    mBitContainer->insertPackedBits(pData);
+    mCodewordReady = true;
+}
+
+void Encoder::setCharCodeword(void* cData)
+{
+    mBitContainer->insertCharBits(cData);
+    mCodewordReady = true;
+}
+
+void Encoder::setFloatCodeword(void* fData)
+{
+    mBitContainer->insertLlr(static_cast<float*>(fData));
+    mCodewordReady = true;
+}
+
+void Encoder::getEncodedData(void* pData) { mBitContainer->getPackedBits(pData); }
+
+void Encoder::clearFrozenBits() { mBitContainer->resetFrozenBits(); }
+
+void Encoder::encode_vector(void* pInfo, void* pCode)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    setInformation(pInfo);
+    encode();
+    getEncodedData(pCode);
+    mEncoderDuration =
+        (size_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+}
+
+UndefinedEncoder::UndefinedEncoder() {}
+
+UndefinedEncoder::~UndefinedEncoder() {}
+
+void UndefinedEncoder::initialize(size_t, const std::vector<unsigned>&) {}
+
+void UndefinedEncoder::encode() { std::fprintf(stderr, "Call to UndefinedEncoder::encode()!\n"); }
+
+ButterflyFipPacked::ButterflyFipPacked() {}
+
+ButterflyFipPacked::ButterflyFipPacked(size_t blockLength) { initialize(blockLength, {}); }
 
 ButterflyFipPacked::ButterflyFipPacked(size_t blockLength, const std::vector<unsigned>& frozenBits)
 {
     initialize(blockLength, frozenBits);
 }
 
+ButterflyFipPacked::~ButterflyFipPacked() {}
+
 void ButterflyFipPacked::initialize(size_t blockLength, const std::vector<unsigned>& frozenBits)
 {
     mBlockLength = blockLength;
     mFrozenBits.assign(frozenBits.begin(), frozenBits.end());
-    mIsFrozen.assign(blockLength, 0);
-    for (unsigned v : mFrozenBits)
-        if (v < blockLength)
-            mIsFrozen[v] = 1;
+    delete mBitContainer;
+    mBitContainer = new PackedContainer(mBlockLength, mFrozenBits);
 }
 
-static void transform(std::vector<uint8_t>& x)
+// butterfly_fip_packed.cpp:45-59: the detector's check bits into the caller's bytes, the
+// bits into the container, transform; systematic: clear the frozen bits, transform again
+void ButterflyFipPacked::encode()
 {
-    const size_t N = x.size();
-    for (size_t B = 1; B < N; B <<= 1)
-        for (size_t j = 0; j < N; j += 2 * B)
-            for (size_t i = j; i < j + B; ++i)
-                x[i] ^= x[i + B];
-}
-
-void ButterflyFipPacked::encode_vector(void* pInfo, void* pCode)
-{
-    const size_t N = mBlockLength, K = infoLength();
-    std::vector<uint8_t> d(static_cast<uint8_t*>(pInfo), static_cast<uint8_t*>(pInfo) + (K + 7) / 8);
-    mErrorDetector->generate(d.data(), (int)(K / 8)); // butterfly_fip_packed.cpp:47-48
-    std::memcpy(pInfo, d.data(), d.size());
-    std::vector<uint8_t> u(N, 0);
-    for (size_t i = 0, j = 0; i < N; ++i)
-        if (!mIsFrozen[i]) {
-            u[i] = (d[j / 8] >> (7 - j % 8)) & 1u;
-            ++j;
-        }
-    transform(u);
-    if (mSystematic) {
-        for (size_t i = 0; i < N; ++i)
-            if (mIsFrozen[i])
-                u[i] = 0;
-        transform(u);
+    if (!mCodewordReady) {
+        mErrorDetector->generate(xmInputData, (int)((mBlockLength - mFrozenBits.size()) / 8));
+        mBitContainer->insertPackedInformationBits(xmInputData);
     }
-    uint8_t* c = static_cast<uint8_t*>(pCode);
-    std::memset(c, 0, N / 8);
-    for (size_t i = 0; i < N; ++i)
-        if (u[i])
-            c[i / 8] |= (uint8_t)(0x80u >> (i % 8));
+    transform();
+    if (mSystematic) {
+        mBitContainer->resetFrozenBits();
+        transform();
+    }
+    mCodewordReady = false;
+}
+
+// x[i] ^= x[i + 2^s] for every i with bit s clear, all stages (butterfly_fip.cpp:15-63),
+// over the code's packed MSB-first bytes (the end of the 256-bit buffer when N < 256)
+void ButterflyFipPacked::transform()
+{
+    const size_t N = mBlockLength;
+    auto* pc = static_cast<PackedContainer*>(mBitContainer);
+    unsigned char* x = reinterpret_cast<unsigned char*>(pc->data()) + (std::max<size_t>(256, N) - N) / 8;
+    static const unsigned char kMask[3] = { 0xAA, 0xCC, 0xF0 }; // positions i with bit s clear, s < 3
+    const size_t bytes = N / 8;
+    for (size_t B = 1; B < N; B <<= 1) {
+        if (B < 8) {
+            const unsigned s = (unsigned)__builtin_ctzll(B);
+            for (size_t j = 0; j < bytes; ++j)
+                x[j] ^= (unsigned char)((x[j] << B) & kMask[s]);
+        } else {
+            const size_t b = B / 8;
+            for (size_t j = 0; j < bytes; j += 2 * b)
+                for (size_t k = j; k < j + b; ++k)
+                    x[k] ^= x[k + b];
+        }
+    }
 }
 
 } // namespace Encoding
@@ -325,64 +394,56 @@ void ButterflyFipPacked::encode_vector(void* pInfo, void* pCode)
 // =============================================================== Decoding
 namespace Decoding {
 
-Decoder::Decoder() : mErrorDetector(&ErrorDetection::globalDummyDetector) {}
+Decoder::Decoder()
+    : mDecoderDuration(0), mErrorDetector(&ErrorDetection::globalDummyDetector), mBlockLength(0), mSystematic(true),
+      mLlrContainer(nullptr), mBitContainer(nullptr), mOutputContainer(nullptr), mFrozenBits(),
+      mExternalContainers(false)
+{
+}
 
-Decoder::~Decoder() {}
+Decoder::~Decoder()
+{
+    if (!mExternalContainers) {
+        delete mLlrContainer;
+        delete mBitContainer;
+        delete[] mOutputContainer;
+    }
+}
 
 void Decoder::initialize(size_t blockLength, const std::vector<unsigned>& frozenBits)
 {
     mBlockLength = blockLength;
     mFrozenBits.assign(frozenBits.begin(), frozenBits.end());
-    mLlr.assign(blockLength, 0.0f);
-    mOutputContainer.assign((blockLength - frozenBits.size() + 7) / 8 + 1, 0);
 }
+
+size_t Decoder::blockLength() { return mBlockLength; }
+
+size_t Decoder::infoLength() { return mBlockLength - mFrozenBits.size(); }
+
+BitContainer* Decoder::inputContainer() { return mLlrContainer; }
+
+BitContainer* Decoder::outputContainer() { return mBitContainer; }
+
+unsigned char* Decoder::packedOutput() { return mOutputContainer; }
 
 void Decoder::setSystematic(bool sys) { mSystematic = sys; }
 
+bool Decoder::isSystematic() { return mSystematic; }
+
 void Decoder::setErrorDetection(ErrorDetection::Detector* pDetector) { mErrorDetector = pDetector; }
 
-void Decoder::setSignal(const float* pLlr)
-{
-    std::memcpy(mLlr.data(), pLlr, 4 * mBlockLength);
-    mSignalI8 = false;
-}
+void Decoder::setSignal(const float* pLlr) { mLlrContainer->insertLlr(pLlr); }
 
-void Decoder::setSignal(const char* pLlr)
-{
-    if (mCharContainer) { // CharContainer::insertLlr(const char*): a copy
-        mLlr8.assign(pLlr, pLlr + mBlockLength);
-        mSignalI8 = true;
-        return;
-    }
-    for (size_t i = 0; i < mBlockLength; ++i) // FloatContainer::insertLlr(const char*), bitcontainer.cpp:202-207
-        mLlr[i] = static_cast<float>(pLlr[i]);
-    mSignalI8 = false;
-}
+void Decoder::setSignal(const char* pLlr) { mLlrContainer->insertLlr(pLlr); }
 
 void Decoder::getDecodedInformationBits(void* pData)
 {
-    std::memcpy(pData, mOutputContainer.data(), (mBlockLength - mFrozenBits.size() + 7) / 8);
+    std::memcpy(pData, mOutputContainer, (mBlockLength - mFrozenBits.size() + 7) / 8);
 }
 
-void Decoder::getSoftCodeword(void* pData)
-{
-    if (mSoftCodeword.size() != mBlockLength)
-        throw std::logic_error("no soft codeword: decode() a frame with a Fast-SSC float decoder first");
-    std::memcpy(pData, mSoftCodeword.data(), mBlockLength * sizeof(float));
-}
+void Decoder::getSoftCodeword(void* pData) { mBitContainer->getSoftBits(pData); }
 
-void Decoder::getSoftInformation(void* pData)
-{
-    if (mSoftCodeword.size() != mBlockLength)
-        throw std::logic_error("no soft codeword: decode() a frame with a Fast-SSC float decoder first");
-    std::vector<uint8_t> isf(mBlockLength, 0);
-    for (unsigned f : mFrozenBits)
-        isf[f] = 1;
-    float* out = static_cast<float*>(pData);
-    for (size_t i = 0; i < mBlockLength; ++i) // the LUT order: info positions ascending
-        if (!isf[i])
-            *out++ = mSoftCodeword[i];
-}
+void Decoder::getSoftInformation(void* pData) { mBitContainer->getSoftInformation(pData); }
 
 bool Decoder::decodeBatch(const float* llr, size_t F, uint8_t* info, uint8_t* ok, float*)
 {
@@ -421,9 +482,8 @@ bool Decoder::decode_vector(const float* pLlr, void* pData)
     setSignal(pLlr);
     const bool r = decode();
     getDecodedInformationBits(pData);
-    mDecoderDuration = (size_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-                           std::chrono::steady_clock::now() - t0)
-                           .count();
+    mDecoderDuration =
+        (size_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
     return r;
 }
 
@@ -433,10 +493,45 @@ bool Decoder::decode_vector(const char* pLlr, void* pData)
     setSignal(pLlr);
     const bool r = decode();
     getDecodedInformationBits(pData);
-    mDecoderDuration = (size_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
-                           std::chrono::steady_clock::now() - t0)
-                           .count();
+    mDecoderDuration =
+        (size_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
     return r;
+}
+
+UndefinedDecoder::UndefinedDecoder() {}
+
+UndefinedDecoder::~UndefinedDecoder() {}
+
+bool UndefinedDecoder::decode()
+{
+    std::fprintf(stderr, "Call to UndefinedDecoder::decode()!\n");
+    return false;
+}
+
+void DecodedFloatContainer::getSoftBits(void* pData)
+{
+    if (!mSoft)
+        throw std::logic_error("no soft codeword: this GPU decoder keeps hard decisions only (soft output: "
+                               "Fast-SSC float decoders, N <= 16384)");
+    FloatContainer::getSoftBits(pData);
+}
+
+void DecodedFloatContainer::getSoftInformation(void* pData)
+{
+    if (!mSoft)
+        throw std::logic_error("no soft codeword: this GPU decoder keeps hard decisions only (soft output: "
+                               "Fast-SSC float decoders, N <= 16384)");
+    FloatContainer::getSoftInformation(pData);
+}
+
+void DecodedCharContainer::getSoftBits(void*)
+{
+    throw std::logic_error("no soft codeword: the GPU 8-bit decoders keep hard decisions only");
+}
+
+void DecodedCharContainer::getSoftInformation(void*)
+{
+    throw std::logic_error("no soft codeword: the GPU 8-bit decoders keep hard decisions only");
 }
 
 static void throw_pcg(int rc)
@@ -450,7 +545,7 @@ static void throw_pcg(int rc)
 }
 
 GpuDecoder::GpuDecoder(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits, int device)
-    : mListSize(listSize), mDevice(device)
+    : mListSize(listSize), mDevice(device), mStageDetector(mErrorDetector)
 {
     initialize(blockLength, frozenBits);
 }
@@ -462,6 +557,27 @@ void GpuDecoder::releasePlan()
     if (mPlan)
         pcg_plan_destroy(mPlan);
     mPlan = nullptr;
+}
+
+// the reference decoders' containers (fastssc_avx_float.cpp:933-937, scl_avx_float.cpp:691-693,
+// fastssc_fip_char.cpp:607-613, scl_fip_char.cpp:796-798): float or char input, an output
+// container, (K+7)/8 packed output bytes
+void GpuDecoder::setupContainers()
+{
+    if (!mExternalContainers) {
+        delete mLlrContainer;
+        delete mBitContainer;
+        delete[] mOutputContainer;
+    }
+    mExternalContainers = false;
+    if (mFixed) {
+        mLlrContainer = new CharContainer(mBlockLength, mFrozenBits);
+        mBitContainer = new DecodedCharContainer(mBlockLength, mFrozenBits);
+    } else {
+        mLlrContainer = new FloatContainer(mBlockLength, mFrozenBits);
+        mBitContainer = new DecodedFloatContainer(mBlockLength, mFrozenBits);
+    }
+    mOutputContainer = new unsigned char[(mBlockLength - mFrozenBits.size() + 7) / 8 + 1]();
 }
 
 void GpuDecoder::initialize(size_t blockLength, const std::vector<unsigned>& frozenBits)
@@ -483,33 +599,82 @@ void GpuDecoder::initialize(size_t blockLength, const std::vector<unsigned>& fro
             throw_pcg(rc);
         pcg_plan_destroy(probe);
     }
+    setupContainers();
 }
 
-void GpuDecoder::setSystematic(bool sys) { mSystematic = sys; }
+void GpuDecoder::setSystematic(bool sys)
+{
+    mStageSystematic = sys;
+    if (!mAdaptive) // AdaptiveFloat::setSystematic sets its stages only (adaptive_float.cpp:47-51)
+        mSystematic = sys;
+}
 
 void GpuDecoder::setErrorDetection(ErrorDetection::Detector* pDetector)
 {
     if (ErrorDetection::gpuKind(pDetector) < 0)
         throw std::logic_error("detector " + pDetector->getType() + " cannot be evaluated on the GPU");
-    mErrorDetector = pDetector;
+    mStageDetector = pDetector;
+    if (!mAdaptive) // AdaptiveFloat::setErrorDetection sets its stages only (adaptive_float.cpp:53-57)
+        mErrorDetector = pDetector;
 }
 
 void GpuDecoder::ensurePlan()
 {
-    const int kind = ErrorDetection::gpuKind(mErrorDetector);
-    if (mPlan && kind == mPlanKind && mSystematic == mPlanSys)
+    const int kind = ErrorDetection::gpuKind(mStageDetector);
+    if (mPlan && kind == mPlanKind && mStageSystematic == mPlanSys)
         return;
     releasePlan();
     auto create = mAdaptive ? (mFixed ? pcg_plan_create_adaptive_char : pcg_plan_create_adaptive)
                             : (mFixed ? pcg_plan_create_char : pcg_plan_create);
     const int rc = create(&mPlan, (uint32_t)mBlockLength, (uint32_t)mListSize, mFrozenBits.data(),
-                          (uint32_t)mFrozenBits.size(), mSystematic ? 1 : 0, kind, mDevice);
+                          (uint32_t)mFrozenBits.size(), mStageSystematic ? 1 : 0, kind, mDevice);
     if (rc != 0) {
         mPlan = nullptr;
         throw_pcg(rc);
     }
     mPlanKind = kind;
-    mPlanSys = mSystematic;
+    mPlanSys = mStageSystematic;
+}
+
+// The decoded codeword's hard decisions into the output container: every decoder output is
+// a codeword, so it is the (systematic or not) encoding of the decoded information bits
+// (butterfly_fip_packed.cpp:45-70 on one bit per byte, any N).
+void GpuDecoder::fillHardCodeword()
+{
+    const size_t N = mBlockLength;
+    std::vector<uint8_t> x(N, 0), frozen(N, 0);
+    for (unsigned f : mFrozenBits)
+        frozen[f] = 1;
+    for (size_t i = 0, j = 0; i < N; ++i)
+        if (!frozen[i]) {
+            x[i] = (mOutputContainer[j / 8] >> (7 - j % 8)) & 1u;
+            ++j;
+        }
+    auto transform = [&]() {
+        for (size_t B = 1; B < N; B <<= 1)
+            for (size_t j = 0; j < N; j += 2 * B)
+                for (size_t i = j; i < j + B; ++i)
+                    x[i] ^= x[i + B];
+    };
+    transform();
+    if (mStageSystematic) {
+        for (size_t i = 0; i < N; ++i)
+            if (frozen[i])
+                x[i] = 0;
+        transform();
+    }
+    if (auto* fc = dynamic_cast<DecodedFloatContainer*>(mBitContainer)) {
+        std::vector<float> bits(N);
+        for (size_t i = 0; i < N; ++i)
+            bits[i] = x[i] ? -0.0f : 0.0f;
+        fc->insertLlr(bits.data());
+        fc->setSoft(false);
+    } else {
+        std::vector<char> bits(N);
+        for (size_t i = 0; i < N; ++i)
+            bits[i] = static_cast<char>(x[i] ? -128 : 127); // CharContainer::insertPackedBits' format
+        mBitContainer->insertCharBits(bits.data());
+    }
 }
 
 bool GpuDecoder::decode()
@@ -520,13 +685,19 @@ bool GpuDecoder::decode()
     ensurePlan();
     uint8_t ok = 0;
     int rc;
-    if (mListSize <= 1 && !mFixed && !mAdaptive && !mSignalI8) {
-        mSoftCodeword.resize(mBlockLength);
-        rc = pcg_decode_f32_soft_host(mPlan, mLlr.data(), 1, mOutputContainer.data(), &ok, mSoftCodeword.data());
-        if (rc != 0) {
-            mSoftCodeword.clear();
+    bool soft = false;
+    if (mListSize <= 1 && !mFixed && !mAdaptive) {
+        auto* out = static_cast<DecodedFloatContainer*>(mBitContainer);
+        rc = pcg_decode_f32_soft_host(mPlan, static_cast<FloatContainer*>(mLlrContainer)->data(), 1,
+                                      mOutputContainer, &ok, out->data());
+        if (rc == PCG_E_UNSUPPORTED) // N beyond the soft kernel's LDS: hard decisions only
+            rc = pcg_decode_f32_host(mPlan, static_cast<FloatContainer*>(mLlrContainer)->data(), 1,
+                                     mOutputContainer, &ok, nullptr);
+        else
+            soft = rc == 0;
+        if (rc != 0)
             throw_pcg(rc);
-        }
+        out->setSoft(soft);
     } else {
         // (the adaptive decoders' list stage runs only for failed frames: no carry there)
         const bool carry = mListSize > 1 && !mAdaptive;
@@ -534,10 +705,12 @@ bool GpuDecoder::decode()
         float* mp = carry ? met.data() : nullptr;
         if (carry && (rc = pcg_plan_set_initial_metric(mPlan, mCarry)) != 0)
             throw_pcg(rc);
-        if (mSignalI8)
-            rc = pcg_decode_i8_host(mPlan, mLlr8.data(), 1, mOutputContainer.data(), &ok, mp);
+        if (mFixed)
+            rc = pcg_decode_i8_host(mPlan, reinterpret_cast<const int8_t*>(static_cast<CharContainer*>(
+                                               mLlrContainer)->data()), 1, mOutputContainer, &ok, mp);
         else
-            rc = pcg_decode_f32_host(mPlan, mLlr.data(), 1, mOutputContainer.data(), &ok, mp);
+            rc = pcg_decode_f32_host(mPlan, static_cast<FloatContainer*>(mLlrContainer)->data(), 1,
+                                     mOutputContainer, &ok, mp);
         if (carry)
             (void)pcg_plan_set_initial_metric(mPlan, 0.0f); // batches keep fresh-decoder semantics
         if (rc != 0)
@@ -545,8 +718,9 @@ bool GpuDecoder::decode()
         if (carry)
             mCarry = met[0];
     }
-    mLastOk = ok != 0;
-    return mLastOk;
+    if (!soft)
+        fillHardCodeword();
+    return ok != 0;
 }
 
 bool GpuDecoder::decodeBatch(const float* llr, size_t F, uint8_t* info, uint8_t* ok, float* metrics)
@@ -578,7 +752,7 @@ void GpuDecoder::decodeBatchDevice(const float* llr, size_t F, uint8_t* info, ui
 
 bool GpuDecoder::decodeBatchI8(const int8_t* llr, size_t F, uint8_t* info, uint8_t* ok, float* metrics)
 {
-    if (!mFixed) { // float decoders take 8-bit LLRs as floats
+    if (!mFixed) { // float decoders take 8-bit LLRs as floats (FloatContainer::insertLlr(const char*))
         std::vector<float> f((size_t)F * mBlockLength);
         for (size_t i = 0; i < f.size(); ++i)
             f[i] = static_cast<float>(llr[i]);
@@ -615,7 +789,6 @@ GpuFastSscChar::GpuFastSscChar(size_t blockLength, const std::vector<unsigned>& 
     : GpuDecoder(blockLength, 1, {}, device)
 {
     mFixed = true;
-    mCharContainer = true;
     initialize(blockLength, frozenBits);
 }
 
@@ -623,7 +796,6 @@ GpuSclChar::GpuSclChar(size_t blockLength, size_t listSize, const std::vector<un
     : GpuDecoder(blockLength, listSize, {}, device)
 {
     mFixed = true;
-    mCharContainer = true;
     initialize(blockLength, frozenBits);
 }
 
@@ -633,7 +805,6 @@ GpuAdaptiveChar::GpuAdaptiveChar(size_t blockLength, size_t listSize, const std:
 {
     mAdaptive = true;
     mFixed = true;
-    mCharContainer = true;
     initialize(blockLength, frozenBits);
 }
 
@@ -645,21 +816,114 @@ GpuAdaptiveFloat::GpuAdaptiveFloat(size_t blockLength, size_t listSize, const st
     initialize(blockLength, frozenBits); // validate both stages now (GpuDecoder's ran before mAdaptive)
 }
 
+// AdaptiveMixed (adaptive_mixed.cpp:14-78)
+GpuAdaptiveMixed::GpuAdaptiveMixed(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,
+                                   int device)
+    : mFastDecoder(nullptr), mListDecoder(nullptr), mListSize(listSize)
+{
+    mBlockLength = blockLength;
+    mFrozenBits.assign(frozenBits.begin(), frozenBits.end());
+    mExternalContainers = true;
+    mFastDecoder = new GpuFastSscChar(mBlockLength, mFrozenBits, device);
+    try {
+        mListDecoder = new GpuSclFloat(mBlockLength, mListSize, mFrozenBits, device);
+    } catch (...) {
+        delete mFastDecoder;
+        throw;
+    }
+    // like the reference, no containers of its own: setSignal(const float*) feeds both
+    // stages; inputContainer() is null (the non-virtual setSignal(const char*) is not usable)
+}
+
+GpuAdaptiveMixed::~GpuAdaptiveMixed()
+{
+    delete mFastDecoder;
+    delete mListDecoder;
+}
+
+bool GpuAdaptiveMixed::decode()
+{
+    bool success = mFastDecoder->decode();
+    mOutputContainer = mFastDecoder->packedOutput();
+    mBitContainer = mFastDecoder->outputContainer();
+    if (!success && mListSize > 1) {
+        success = mListDecoder->decode();
+        mOutputContainer = mListDecoder->packedOutput();
+        mBitContainer = mListDecoder->outputContainer();
+    }
+    return success;
+}
+
+void GpuAdaptiveMixed::setSystematic(bool sys)
+{
+    mFastDecoder->setSystematic(sys);
+    mListDecoder->setSystematic(sys);
+}
+
+void GpuAdaptiveMixed::setErrorDetection(ErrorDetection::Detector* pDetector)
+{
+    mFastDecoder->setErrorDetection(pDetector);
+    mListDecoder->setErrorDetection(pDetector);
+}
+
+void GpuAdaptiveMixed::setSignal(const float* pLlr)
+{
+    mFastDecoder->setSignal(pLlr);
+    mListDecoder->setSignal(pLlr);
+}
+
+bool GpuAdaptiveMixed::decodeBatch(const float* llr, size_t F, uint8_t* info, uint8_t* ok, float*)
+{
+    const size_t N = mBlockLength, kb = (infoLength() + 7) / 8;
+    std::vector<uint8_t> okv(F, 0);
+    mFastDecoder->decodeBatch(llr, F, info, okv.data()); // the 8-bit plan quantises (insertLlr)
+    std::vector<size_t> bad;
+    for (size_t f = 0; f < F; ++f)
+        if (!okv[f])
+            bad.push_back(f);
+    if (!bad.empty() && mListSize > 1) {
+        std::vector<float> sub(bad.size() * N);
+        for (size_t i = 0; i < bad.size(); ++i)
+            std::memcpy(&sub[i * N], llr + bad[i] * N, N * sizeof(float));
+        std::vector<uint8_t> si(bad.size() * kb), sk(bad.size());
+        mListDecoder->decodeBatch(sub.data(), bad.size(), si.data(), sk.data());
+        for (size_t i = 0; i < bad.size(); ++i) {
+            std::memcpy(info + bad[i] * kb, &si[i * kb], kb);
+            okv[bad[i]] = sk[i];
+        }
+    }
+    bool all = true;
+    for (size_t f = 0; f < F; ++f) {
+        if (ok)
+            ok[f] = okv[f];
+        all = all && okv[f];
+    }
+    return all;
+}
+
 Decoder* makeDecoder(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits, int impl)
 {
     Decoder* dec;
-    if (impl == 3)
-        throw std::logic_error("decoder implementation 3 (SCAN) is not part of this build (use \"gpu\")");
-    if (listSize <= 1 && impl == 1)
-        dec = new GpuFastSscFloat(blockLength, frozenBits);
-    else if (listSize <= 1)
-        dec = new GpuFastSscChar(blockLength, frozenBits); // decoder.cpp:60-68: default branch
-    else if (impl == 0)
-        dec = new GpuSclChar(blockLength, listSize, frozenBits);
-    else if (impl == 2)
-        dec = new GpuAdaptiveFloat(blockLength, listSize, frozenBits);
-    else
-        dec = new GpuSclFloat(blockLength, listSize, frozenBits);
+    if (listSize == 1) { // decoder.cpp:60-68: 1 -> float, anything else -> 8-bit
+        if (impl == 1)
+            dec = new GpuFastSscFloat(blockLength, frozenBits);
+        else
+            dec = new GpuFastSscChar(blockLength, frozenBits);
+    } else { // decoder.cpp:69-83
+        switch (impl) {
+        case 1:
+            dec = new GpuSclFloat(blockLength, listSize, frozenBits);
+            break;
+        case 2:
+            dec = new GpuAdaptiveFloat(blockLength, listSize, frozenBits);
+            break;
+        case 3:
+            throw std::logic_error("decoder implementation 3 (SCAN) is not part of this build");
+        default:
+            dec = new GpuSclChar(blockLength, listSize, frozenBits);
+            break;
+        }
+    }
     dec->setErrorDetection(new ErrorDetection::CRC8()); // decoder.cpp:85 (never freed there either)
     return dec;
 }

@@ -36,10 +36,9 @@ struct KernelArgs {
     // 8-bit ("char") plans: F x N int8 channel LLRs; null -> `llr` floats are quantised
     // in the kernel exactly as CharContainer::insertLlr does
     const int8_t* llr8;
-    // persistent lane-serial kernels: two zeroed device counters [next group, waves done];
-    // waves take codeword groups from counter 0 (dynamic balance across SIMDs whose wave
-    // counts differ) and the last wave to finish zeroes both for the next launch.
-    // null -> static grid-stride assignment.
+    // persistent lane-serial kernels: a device counter the caller zeroes on the launch
+    // stream before every launch (capi.cpp); waves take codeword groups from it (dynamic
+    // balance across SIMDs whose wave counts differ).  null -> static grid-stride assignment.
     uint32_t* queue;
     // grid size (persistent waves) chosen by the caller: min(groups, the plan's wave cap)
     uint32_t units;
@@ -68,24 +67,14 @@ inline uint64_t env_wpc(const char* name, uint64_t dflt)
 
 // Dynamic group assignment for the persistent lane-serial kernels (KernelArgs::queue;
 // one-wave workgroups). Every lane gets the same ticket; a wave stops at its first ticket
-// past the last group, and the wave that retires last resets the counters (every other
-// wave has taken its final ticket by then, so nothing touches counter 0 after the reset).
+// past the last group.  The counter is reset by a hipMemsetAsync on the launch stream
+// before each launch, so an aborted launch or another stream cannot leave it dirty.
 __device__ inline uint64_t queue_next(uint32_t* q)
 {
     uint32_t t = 0;
     if (__lane_id() == 0)
         t = __hip_atomic_fetch_add(q, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-}
-__device__ inline void queue_retire(uint32_t* q)
-{
-    if (__lane_id() == 0) {
-        const uint32_t d = __hip_atomic_fetch_add(q + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (d == gridDim.x - 1) {
-            __hip_atomic_store(q, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(q + 1, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
 }
 
 // LDS floats one SC codeword needs: alpha (N floats, index 0 unused) + packed bits.

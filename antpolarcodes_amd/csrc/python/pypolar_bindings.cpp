@@ -9,6 +9,7 @@
 
 #include <polarcode/construction/constructor.h>
 #include <polarcode/decoding/decoder.h>
+#include <polarcode/encoding/butterfly_fip_packed.h>
 #include <polarcode/encoding/encoder.h>
 #include <polarcode/errordetection/errordetector.h>
 #include <polarcode/puncturer.h>

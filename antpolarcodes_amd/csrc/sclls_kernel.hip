@@ -1645,8 +1645,6 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
         }
 #endif
     }
-    if (a.queue)
-        queue_retire(a.queue);
 #ifdef PCG_LS_PROF
     wsync();
     if (c.lane == 0 && a.prof)

@@ -271,6 +271,11 @@ class GpuBackend:
         self.scale = job.amplification * self.sigma * self.sigma / 2.0
 
     def frames(self, job, F, seed):
+        # a worker thread starts on cuda:0: events, streams and syncs must be this worker's GPU's
+        with self.torch.cuda.device(self.dev):
+            return self._frames(job, F, seed)
+
+    def _frames(self, job, F, seed):
         torch = self.torch
         from ._native import bpsk_awgn_device, random_info_device
         kb = (job.K + 7) // 8
@@ -278,22 +283,28 @@ class GpuBackend:
         code = torch.empty((F, job.N // 8), dtype=torch.uint8, device=self.dev)
         llr = torch.empty((F, job.N), dtype=torch.float32, device=self.dev)
         random_info_device(info, job.K, seed)
+        st = torch.cuda.current_stream(self.dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
+        e0.record(st)
         self.enc.encode_device(info, code)
-        e1.record()
+        e1.record(st)
         bpsk_awgn_device(code, job.N, self.sigma, seed ^ 0x9E3779B97F4A7C15, llr)
         llr.mul_(self.scale)
-        torch.cuda.synchronize()
+        torch.cuda.synchronize(self.dev)
         return llr, info, e0.elapsed_time(e1) * 1e-3
 
     def decode(self, job, llr):
+        with self.torch.cuda.device(self.dev):
+            return self._decode(job, llr)
+
+    def _decode(self, job, llr):
         torch = self.torch
         F = llr.shape[0]
         out = torch.empty((F, self.plan.kb), dtype=torch.uint8, device=self.dev)
         ok = torch.empty(F, dtype=torch.uint8, device=self.dev)
+        st = torch.cuda.current_stream(self.dev)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
+        e0.record(st)
         self.plan.decode_device(llr, out, ok)  # 8-bit plans quantise the floats (insertLlr)
         if self.second is not None:  # AdaptiveMixed: list decoding of the failed frames
             bad = torch.nonzero(ok == 0).flatten()
@@ -304,8 +315,8 @@ class GpuBackend:
                 self.second.decode_device(sub, so, sk)
                 out.index_copy_(0, bad, so)
                 ok.index_copy_(0, bad, sk)
-        e1.record()
-        torch.cuda.synchronize()
+        e1.record(st)
+        torch.cuda.synchronize(self.dev)
         return out.cpu().numpy(), ok.cpu().numpy(), e0.elapsed_time(e1) * 1e-3
 
     def close(self):

@@ -477,6 +477,9 @@ def main(argv=None):
             "roofline": roof,
             "src_digest": digest,
         }
+        # developer environment switches that changed the plan (pcg_plan_desc.dev_overrides):
+        # 0 = the production kernel and layout
+        line["config"]["dev_overrides"] = plan.describe()["dev_overrides"]
         head = git_head()
         if head:
             line["git_head"] = head

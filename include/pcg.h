@@ -51,12 +51,14 @@
  * nothing throws across the ABI.  pcg_last_error() (thread-local) describes the
  * most recent failure on the calling thread.
  *
- * Threading: a plan is like the reference's stateful Decoder objects (one per
- * worker thread, simulator.cpp:703-764): its scratch, work queue, staging and
- * adaptive frame-map buffers are reused by every decode call, so all decode entry
- * points on one plan must be issued from one host thread on one stream (calls on
- * one stream are ordered; two streams would race on the plan's buffers).  Plans are
- * independent of each other: one plan per stream / per GPU runs concurrently.
+ * Threading and streams: a plan is like the reference's stateful Decoder objects (one per
+ * worker thread, simulator.cpp:703-764): its scratch, work queue, staging and adaptive
+ * frame-map buffers are reused by every decode call, so a plan must be used from one host
+ * thread at a time.  Decodes of one plan may be issued on different streams: each decode
+ * waits (hipStreamWaitEvent) for the plan's previous decode, whichever stream ran it, so
+ * they never overlap; the SCL work-queue counter is zeroed on the launch stream before
+ * every launch; pcg_plan_destroy waits for the plan's last decode before freeing.  Plans
+ * are independent of each other: one plan per stream / per GPU runs concurrently.
  */
 #ifndef PCG_H
 #define PCG_H
@@ -97,7 +99,18 @@ typedef struct pcg_plan_desc {
     uint64_t scratch_bytes; /* global scratch per codeword */
     int32_t crc_kind;
     int32_t systematic;
+    uint32_t lanes_per_codeword; /* SCL: lanes of a wave per codeword (list size rounded up, or
+                                    wider); Fast-SSC scq kernel: its Q; 0 for the other kernels */
+    uint32_t dev_overrides;      /* PCG_DEV_* bits: developer environment switches
+                                    that changed this plan's kernel or layout; 0 in production */
 } pcg_plan_desc;
+
+#define PCG_DEV_SCL_LP 0x1   /* PCG_SCL_LP / PCG_ADAPT_LP (only when the caller passed 0) */
+#define PCG_DEV_SCL_FUSE 0x2 /* PCG_SCL_FUSE */
+#define PCG_DEV_SCQ 0x4      /* PCG_SCQ_Q / PCG_SCQ_VIRT */
+#define PCG_DEV_LAYOUT 0x8   /* PCG_SC_KERNEL, PCG_*_LDS_KB, PCG_*_SL, PCG_*_WPC, PCG_SCL_VIRT, ... */
+#define PCG_DEV_OPPROF 0x10  /* PCG_OPPROF */
+#define PCG_DEV_FLAGS 0x20   /* PCG_FLAGS */
 
 /* Build a decoding plan: classify the decoder tree exactly as the reference
  * (Fast-SSC for L == 1, SCL for L >= 2), flatten it to a device schedule and
@@ -272,7 +285,7 @@ void pcg_puncturer_destroy(pcg_puncturer* punc);
 /* Decode F punctured frames: llr is F x E (device), depunctured on the device into the
  * plan's staging buffer and decoded with `plan` (whose N must equal the puncturer's
  * parent length).  Outputs as pcg_decode_f32.  Stream-ordered; the staging buffer is
- * reused across calls on the same plan, so calls on one plan must share one stream. */
+ * reused across calls on the same plan (ordered after the plan's previous decode). */
 int pcg_decode_punctured_f32(pcg_plan* plan,
                              const pcg_puncturer* punc,
                              const float* llr,

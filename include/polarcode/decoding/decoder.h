@@ -2,11 +2,14 @@
 // PolarCode::Decoding -- drop-in for the reference's decoder interface
 // (include/polarcode/decoding/decoder.h:40-211 of david13pod/antPolarCodes).
 //
-// The virtual base keeps the reference's names, argument meanings and error
-// behaviour; the implementations (GpuFastSscFloat, GpuSclFloat) run the
-// MI355X kernels through the C ABI of include/pcg.h.  New: decodeBatch() for F
-// frames per call (host buffers) and decodeBatchDevice() (device buffers,
-// asynchronous on a HIP stream).
+// The virtual base keeps the reference's members, names, argument meanings and error
+// behaviour (BitContainer input/output containers, unsigned char* packed output,
+// mExternalContainers), so reference-style subclasses compile unchanged.  The
+// implementations (GpuFastSscFloat, GpuSclFloat, ... -- also reachable under the
+// reference's class names through <polarcode/decoding/fastssc_avx_float.h> etc.) run the
+// MI355X kernels through the C ABI of include/pcg.h.  New: decodeBatch() for F frames per
+// call (host buffers), decodeBatchDevice() (device buffers, asynchronous on a HIP stream)
+// and decodeBatchI8().
 #ifndef PCA_DECODER_H
 #define PCA_DECODER_H
 
@@ -15,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include <polarcode/bitcontainer.h>
 #include <polarcode/errordetection/errordetector.h>
 
 struct pcg_plan;
@@ -22,67 +26,63 @@ struct pcg_plan;
 namespace PolarCode {
 namespace Decoding {
 
+enum DecoderType { tFlexible, tFixed, tDepthFirst, tScan, tFastSscan };
+
 class Decoder
 {
+private:
+    size_t mDecoderDuration;
+
 protected:
-    size_t mDecoderDuration = 0;
-    ErrorDetection::Detector* mErrorDetector; ///< not owned (as in the reference)
-    size_t mBlockLength = 0;
-    bool mSystematic = true;
-    std::vector<unsigned> mFrozenBits;
-    std::vector<float> mLlr;                  ///< setSignal() input (one frame)
-    std::vector<int8_t> mLlr8;                ///< setSignal(const char*) input of 8-bit decoders
-    bool mSignalI8 = false;                   ///< the pending frame is mLlr8
-    std::vector<unsigned char> mOutputContainer;
-    bool mLastOk = false;
-    bool mCharContainer = false;              ///< 8-bit decoder: setSignal(const char*) keeps the bytes
-    std::vector<float> mSoftCodeword;         ///< soft codeword of the last decode() (empty: none)
+    ErrorDetection::Detector* mErrorDetector; ///< Error detecting object (not owned)
+    size_t mBlockLength;                      ///< Length of the Polar Code
+    bool mSystematic;                         ///< Whether to use systematic coding
+    BitContainer* mLlrContainer;              ///< Soft-input container
+    BitContainer* mBitContainer;              ///< (optionally soft-) Output bit container
+    unsigned char* mOutputContainer;          ///< Decoded information bytes, (K+7)/8
+    std::vector<unsigned> mFrozenBits;        ///< Indices for frozen bits
+    bool mExternalContainers;                 ///< On destruction, do not delete containers
 
 public:
     Decoder();
     virtual ~Decoder();
 
-    /// Decode the frame given by setSignal(); returns the detector's verdict.
+    /// Decode the signal given by setSignal(); returns the detector's verdict.
     virtual bool decode() = 0;
     /// setSignal + decode + getDecodedInformationBits (decoder.cpp:154-167).
     bool decode_vector(const float* pLlr, void* pData);
     /// setSignal(const char*) + decode + getDecodedInformationBits (decoder.cpp:169-181).
     bool decode_vector(const char* pLlr, void* pData);
+    /// Nanoseconds of the last decode_vector call.
     size_t duration_ns() { return mDecoderDuration; }
 
     virtual void initialize(size_t blockLength, const std::vector<unsigned>& frozenBits);
     std::vector<unsigned> frozenBits() { return mFrozenBits; }
-    size_t blockLength() { return mBlockLength; }
-    size_t infoLength() { return mBlockLength - mFrozenBits.size(); }
-    unsigned char* packedOutput() { return mOutputContainer.data(); }
+    size_t blockLength();
+    size_t infoLength();
+
+    BitContainer* inputContainer();  ///< mLlrContainer
+    BitContainer* outputContainer(); ///< mBitContainer
+    unsigned char* packedOutput();   ///< mOutputContainer
 
     virtual void setSystematic(bool sys);
-    bool isSystematic() { return mSystematic; }
+    bool isSystematic();
     virtual void setErrorDetection(ErrorDetection::Detector* pDetector);
     std::string getErrorDetectionMode()
     {
-        return mErrorDetector->getType() + "-" + std::to_string(mErrorDetector->getCheckBitCount());
+        return std::string(mErrorDetector->getType() + "-" + std::to_string(mErrorDetector->getCheckBitCount()));
     }
     virtual size_t getListSize() { return 1; }
+    /// mLlrContainer->insertLlr(pLlr) (decoder.cpp:138).
     virtual void setSignal(const float* pLlr);
-    /// 8-bit LLRs (non-virtual, as in the reference, decoder.h:170): float decoders convert
-    /// them (FloatContainer::insertLlr(const char*), bitcontainer.cpp:202-207); 8-bit
-    /// decoders take them as they are (CharContainer::insertLlr).
+    /// mLlrContainer->insertLlr(pLlr) (decoder.cpp:140): float containers convert the
+    /// bytes, char containers copy them.
     void setSignal(const char* pLlr);
     void getDecodedInformationBits(void* pData);
-    /// The last decode()'s soft codeword, N floats (FloatContainer::getSoftBits,
-    /// bitcontainer.cpp:294-297): the root bit container word for word.  Available from
-    /// the Fast-SSC float decoder; std::logic_error for decoders whose GPU kernels keep
-    /// hard decisions only (SCL, 8-bit, adaptive).
+    /// mBitContainer->getSoftBits (decoder.cpp:147).
     void getSoftCodeword(void* pData);
-    /// The soft codeword at the information positions, K floats
-    /// (FloatContainer::getSoftInformation, bitcontainer.cpp:331-339).
+    /// mBitContainer->getSoftInformation (decoder.cpp:149-152).
     void getSoftInformation(void* pData);
-    /// Direct access to the decoder's input LLRs (N floats) and soft output (N floats,
-    /// empty before a soft-capable decode).  The reference returns its BitContainer
-    /// objects here (decoder.h:107-108); this build has no container classes.
-    float* inputContainer() { return mLlr.data(); }
-    float* outputContainer() { return mSoftCodeword.empty() ? nullptr : mSoftCodeword.data(); }
 
     /// Batched decode of F frames (host memory): llr F x N, info F x ceil(K/8),
     /// ok F (nullable), metrics F x L (nullable, list decoders only).  Returns true if
@@ -99,6 +99,42 @@ public:
                                float* metrics = nullptr);
 };
 
+class UndefinedDecoder : public Decoder
+{
+public:
+    UndefinedDecoder();
+    ~UndefinedDecoder();
+    bool decode() override;
+};
+
+/// Output container of the GPU float decoders (outputContainer()): after a Fast-SSC float
+/// decode (N <= 16384) it holds the soft codeword word for word (FloatContainer::getSoftBits
+/// of the reference); otherwise the decoded codeword's hard decisions as sign bits
+/// (+0.0 / -0.0) -- getPackedBits / getFloatBits / getPackedInformationBits exact -- and
+/// the soft accessors raise std::logic_error (the list, 8-bit and adaptive kernels keep
+/// hard decisions only).
+class DecodedFloatContainer : public FloatContainer
+{
+    bool mSoft = false;
+
+public:
+    DecodedFloatContainer(size_t size, const std::vector<unsigned>& frozenBits) : FloatContainer(size, frozenBits) {}
+    void setSoft(bool soft) { mSoft = soft; }
+    bool isSoft() const { return mSoft; }
+    void getSoftBits(void* pData) override;
+    void getSoftInformation(void* pData) override;
+};
+
+/// Output container of the GPU 8-bit decoders: hard decisions as char bits (0 -> 127,
+/// 1 -> -128, CharContainer::insertPackedBits); soft accessors raise std::logic_error.
+class DecodedCharContainer : public CharContainer
+{
+public:
+    DecodedCharContainer(size_t size, const std::vector<unsigned>& frozenBits) : CharContainer(size, frozenBits) {}
+    void getSoftBits(void* pData) override;
+    void getSoftInformation(void* pData) override;
+};
+
 /// Shared GPU plumbing: owns one pcg_plan, rebuilt when code / detector / systematic
 /// flag change.
 class GpuDecoder : public Decoder
@@ -111,11 +147,18 @@ protected:
     bool mPlanSys = true;
     bool mAdaptive = false; ///< pcg_plan_create_adaptive (Fast-SSC first, SCL for failures)
     bool mFixed = false;    ///< pcg_plan_create_char (the reference's 8-bit decoders)
+    /// the detector / systematic flag the plan evaluates: mErrorDetector / mSystematic,
+    /// except for the adaptive decoders, which (as AdaptiveFloat, adaptive_float.cpp:47-57)
+    /// pass them to their stages and leave their own members untouched
+    ErrorDetection::Detector* mStageDetector;
+    bool mStageSystematic = true;
     /// SCL: path 0's final metric of the last decode(), the next decode()'s start metric --
     /// one reference decoder instance reused frame after frame
     float mCarry = 0.0f;
     void ensurePlan();
     void releasePlan();
+    void setupContainers();
+    void fillHardCodeword();
 
 public:
     GpuDecoder(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits, int device);
@@ -150,26 +193,22 @@ public:
     }
 };
 
-/// CRC-aided SCL (SclAvxFloat, scl_avx_float.cpp) on the GPU; listSize 2..32.
+/// CRC-aided SCL (SclAvxFloat, scl_avx_float.cpp) on the GPU; listSize 2..32 (any value).
 class GpuSclFloat : public GpuDecoder
 {
 public:
-    GpuSclFloat(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,
-                int device = 0)
+    GpuSclFloat(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits, int device = 0)
         : GpuDecoder(blockLength, listSize, frozenBits, device)
     {
     }
 };
 
-/// makeDecoder (decoder.cpp:54-87): L == 1 -> Fast-SSC, else SCL; always installs
-/// a CRC-8 detector (the reference's Q5 behaviour).
-/// AdaptiveFloat (adaptive_float.cpp:14-45): Fast-SSC, then CRC-aided SCL for the frames
+/// AdaptiveFloat (adaptive_float.cpp:14-57): Fast-SSC, then CRC-aided SCL for the frames
 /// whose check fails -- per frame, on the GPU, in one batched call.
 class GpuAdaptiveFloat : public GpuDecoder
 {
 public:
-    GpuAdaptiveFloat(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,
-                     int device = 0);
+    GpuAdaptiveFloat(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits, int device = 0);
 };
 
 /// FastSscFipChar (fastssc_fip_char.cpp) on the GPU: 8-bit saturating LLRs.
@@ -195,15 +234,40 @@ public:
                     int device = 0);
 };
 
-/// decoder_impl as in decoder.cpp:54-87: 0 = char (FastSscFipChar / SclFipChar), 1 = float
-/// (Fast-SSC / SCL), 2 = AdaptiveFloat (list size >= 2); SCAN (3) is not part of this build.
-Decoder* makeDecoder(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,
-                     int decoder_impl = 1);
+/// AdaptiveMixed (adaptive_mixed.cpp:14-78; pcsim's default precision 832): FastSscFipChar
+/// over the (quantised) float frames, then the float SCL for the frames whose check fails.
+/// Composed of two GPU decoders like the reference composes two CPU ones.
+class GpuAdaptiveMixed : public Decoder
+{
+    GpuFastSscChar* mFastDecoder;
+    GpuSclFloat* mListDecoder;
+    size_t mListSize;
 
-/// create (decoder.cpp:26-52).  "gpu" and "float" select the MI355X float decoders
-/// (listSize < 2 -> Fast-SSC), "char" the 8-bit ones, "mixed" AdaptiveFloat; "scan" is a
-/// reference decoder outside this build and raises std::logic_error; unknown strings raise
-/// std::logic_error("Unknown PolarDecoder type!") exactly as the reference.
+public:
+    GpuAdaptiveMixed(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,
+                     int device = 0);
+    ~GpuAdaptiveMixed() override;
+    bool decode() override;
+    void setSystematic(bool sys) override;
+    void setErrorDetection(ErrorDetection::Detector* pDetector) override;
+    void setSignal(const float* pLlr) override;
+    size_t getListSize() override { return mListSize; }
+    /// Fast stage over all frames, list stage over the failures (host buffers).
+    bool decodeBatch(const float* llr, size_t F, uint8_t* info, uint8_t* ok = nullptr,
+                     float* metrics = nullptr) override;
+};
+
+/// makeDecoder (decoder.cpp:54-87): decoder_impl 1 = float (Fast-SSC for listSize 1, else
+/// SCL), 2 = AdaptiveFloat (listSize >= 2), 3 = SCAN (not part of this build:
+/// std::logic_error), every other value = the 8-bit decoders (FastSscFipChar / SclFipChar),
+/// the default 0 included.  Always installs a CRC-8 detector (the reference's Q5 behaviour).
+Decoder* makeDecoder(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,
+                     int decoder_impl = 0);
+
+/// create (decoder.cpp:26-52).  "char" -> 8-bit, "float" (and this build's "gpu") -> the
+/// MI355X float decoders, "mixed" -> AdaptiveFloat; listSize < 2 turns every non-char type
+/// into Fast-SSC float; "scan" is outside this build (std::logic_error); unknown strings
+/// raise std::logic_error("Unknown PolarDecoder type!") exactly as the reference.
 Decoder* create(size_t blockLength, size_t listSize, const std::vector<unsigned>& frozenBits,
                 std::string decoderType);
 

@@ -1,15 +1,19 @@
 /* -*- c++ -*- */
-// PolarCode::Encoding::Encoder (encoder.h:24-151 of the reference) and the packed
-// butterfly encoder (butterfly_fip_packed.cpp:45-70), host-side.  Used to build
-// frames and by callers that pair it with the GPU decoders.
+// PolarCode::Encoding::Encoder -- the reference's encoder skeleton-class
+// (include/polarcode/encoding/encoder.h:24-151, src/polarcode/encoding/encoder.cpp of
+// david13pod/antPolarCodes), unchanged in members and semantics: encode() is the pure
+// virtual algorithm, encode_vector() = setInformation + encode + getEncodedData, the
+// bits live in a BitContainer (include/polarcode/bitcontainer.h).  ButterflyFipPacked
+// is in <polarcode/encoding/butterfly_fip_packed.h>; the batched device encoder is
+// pcg_encode (include/pcg.h).
 #ifndef PCA_ENCODER_H
 #define PCA_ENCODER_H
 
 #include <cstddef>
-#include <cstdint>
 #include <string>
 #include <vector>
 
+#include <polarcode/bitcontainer.h>
 #include <polarcode/errordetection/errordetector.h>
 
 namespace PolarCode {
@@ -17,39 +21,68 @@ namespace Encoding {
 
 class Encoder
 {
+private:
+    size_t mEncoderDuration;
+
 protected:
-    ErrorDetection::Detector* mErrorDetector;
-    size_t mBlockLength;
-    bool mSystematic;
-    std::vector<unsigned> mFrozenBits;
+    ErrorDetection::Detector* mErrorDetector; ///< Error detecting object (not owned)
+    size_t mBlockLength;                      ///< Block length of the Polar Code
+    bool mSystematic;                         ///< Whether to use systematic coding
+    bool mCodewordReady;                      ///< mBitContainer already holds the bits to encode
+    unsigned char* xmInputData;               ///< Bits to encode (setInformation / setCodeword)
+    BitContainer* mBitContainer;              ///< Internal bit memory (owned)
+    std::vector<unsigned> mFrozenBits;        ///< Indices for frozen bits
 
 public:
     Encoder();
-    virtual ~Encoder() {}
-    virtual void encode_vector(void* pInfo, void* pCode) = 0;
+    virtual ~Encoder();
+    virtual void encode() = 0; ///< Execute the encoding algorithm.
+
+    /// setInformation(pInfo) + encode() + getEncodedData(pCode) (encoder.cpp:79-90).
+    void encode_vector(void* pInfo, void* pCode);
+
+    /// Nanoseconds of the last encoder call (never set by the reference's encode_vector).
+    size_t duration_ns() { return mEncoderDuration; }
+
     virtual void initialize(size_t blockLength, const std::vector<unsigned>& frozenBits) = 0;
-    size_t blockLength() { return mBlockLength; }
-    size_t infoLength() { return mBlockLength - mFrozenBits.size(); }
+
+    size_t infoLength() { return blockLength() - mFrozenBits.size(); }
+    size_t blockLength();
     std::vector<unsigned> frozenBits() { return mFrozenBits; }
-    void setErrorDetection(ErrorDetection::Detector* pDetector) { mErrorDetector = pDetector; }
+
+    void setErrorDetection(ErrorDetection::Detector* pDetector);
     std::string getErrorDetectionMode()
     {
-        return mErrorDetector->getType() + "-" + std::to_string(mErrorDetector->getCheckBitCount());
+        return std::string(mErrorDetector->getType() + "-" + std::to_string(mErrorDetector->getCheckBitCount()));
     }
-    void setSystematic(bool sys) { mSystematic = sys; }
-    bool isSystematic() { return mSystematic; }
+
+    void setSystematic(bool sys);
+    bool isSystematic();
+
+    /// Keep a pointer to the packed information bytes for the next encode() (not copied;
+    /// encode() writes the detector's check bits into them, as the reference does).
+    void setInformation(void* pData);
+    /// Packed information bits of the container (after encode(): of the codeword).
+    void getInformation(void* pData);
+    /// Packed codeword bits into the container; the next encode() transforms them as given.
+    void setCodeword(void* pData);
+    /// Char bits (MSB of each byte) into the container.
+    void setCharCodeword(void* cData);
+    /// Float bits (sign bits) into the container.
+    void setFloatCodeword(void* fData);
+    /// Packed code bits (N/8 bytes) of the last encode().
+    void getEncodedData(void* pData);
+    /// Set all frozen bits to 0.
+    void clearFrozenBits();
 };
 
-/// ButterflyFipPacked: info bytes (MSB-first, CRC generated over them first) ->
-/// packed codeword bytes; systematic = transform, clear frozen, transform.
-class ButterflyFipPacked : public Encoder
+class UndefinedEncoder : public Encoder
 {
-    std::vector<uint8_t> mIsFrozen;
-
 public:
-    ButterflyFipPacked(size_t blockLength, const std::vector<unsigned>& frozenBits);
-    void initialize(size_t blockLength, const std::vector<unsigned>& frozenBits) override;
-    void encode_vector(void* pInfo, void* pCode) override;
+    UndefinedEncoder();
+    ~UndefinedEncoder();
+    void initialize(size_t, const std::vector<unsigned>&) override;
+    void encode() override;
 };
 
 } // namespace Encoding

@@ -1,13 +1,16 @@
-// A Decoder subclass written the way the reference's own decoders are (override decode()
-// only, use setSignal / decode_vector / getDecodedInformationBits from the base), compiled
+// A Decoder subclass written the way the reference's own decoders are (containers created in
+// initialize(), decode() reads mLlrContainer and fills mOutputContainer, the base's
+// setSignal / decode_vector / getDecodedInformationBits / destructor do the rest), compiled
 // against this build's include/polarcode/decoding/decoder.h and linked with
 // libpolarcode_amd.so.  Checks that the base class keeps the reference's contract: the
 // batch methods have working defaults, setSignal(const char*) converts bytes for float
-// decoders, the soft-output accessors fail loudly when no soft codeword exists, and the
-// GPU factory validates codes without a GPU.  (tests/test_cpp_boundary.py builds and runs it.)
+// containers, the containers are BitContainers, and the GPU factory validates codes without a
+// GPU.  (tests/test_cpp_boundary.py builds and runs it.)
+#include <polarcode/bitcontainer.h>
 #include <polarcode/decoding/decoder.h>
 #include <polarcode/errordetection/errordetector.h>
 
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
@@ -20,11 +23,20 @@ class SignDecoder : public Decoding::Decoder
 {
 public:
     SignDecoder(size_t n, const std::vector<unsigned>& frozen) { initialize(n, frozen); }
+    void initialize(size_t n, const std::vector<unsigned>& frozen) override
+    {
+        Decoder::initialize(n, frozen);
+        mLlrContainer = new FloatContainer(n);
+        mBitContainer = new FloatContainer(n, frozen);
+        mOutputContainer = new unsigned char[(n - frozen.size() + 7) / 8];
+    }
     bool decode() override
     {
-        const unsigned char b = mLlr[0] < 0.0f ? 0xff : 0x00;
-        std::memset(mOutputContainer.data(), b, mOutputContainer.size());
-        return mLlr[0] != 0.0f;
+        const float* llr = static_cast<FloatContainer*>(mLlrContainer)->data();
+        const unsigned char b = llr[0] < 0.0f ? 0xff : 0x00;
+        std::memset(mOutputContainer, b, infoLength() / 8);
+        mBitContainer->insertPackedInformationBits(mOutputContainer);
+        return llr[0] != 0.0f;
     }
 };
 
@@ -48,17 +60,28 @@ int main()
     llr[16] = -2.0f; // frame 1 negative
     llr[32] = 0.0f;  // frame 2 "fails"
     unsigned char one = 0;
-    CHECK(d.decode_vector(llr.data() + 16, &one) && one == 0xff);
+    CHECK(d.decode_vector(llr.data() + 16, &one) && one == 0xff && d.packedOutput()[0] == 0xff);
     std::vector<uint8_t> info(3), ok(3);
     CHECK(!d.decodeBatch(llr.data(), 3, info.data(), ok.data()));
     CHECK(info[0] == 0x00 && info[1] == 0xff && ok[0] == 1 && ok[1] == 1 && ok[2] == 0);
-    // setSignal(const char*) is the base's non-virtual conversion for float decoders
+    // setSignal(const char*) is the base's non-virtual conversion through the FloatContainer
     std::vector<char> c8(16, 5);
     c8[0] = -3;
-    CHECK(d.decode_vector(c8.data(), &one) && one == 0xff && d.inputContainer()[0] == -3.0f);
+    CHECK(d.decode_vector(c8.data(), &one) && one == 0xff);
+    std::vector<float> frame(16);
+    d.inputContainer()->getSoftBits(frame.data());
+    CHECK(frame[0] == -3.0f && frame[1] == 5.0f);
     std::vector<int8_t> b8(2 * 16, 1);
     CHECK(d.decodeBatchI8(b8.data(), 2, info.data(), ok.data()) && info[0] == 0);
-    // the device batch and soft outputs are not available on a CPU decoder: loud failures
+    // the output container is a BitContainer: packed bits / soft information as the reference
+    d.decode_vector(llr.data() + 16, &one);
+    unsigned char packed[2] = { 0, 0 };
+    d.outputContainer()->getPackedBits(packed);
+    CHECK(packed[0] == 0x00 && packed[1] == 0xff);
+    std::vector<float> si(8);
+    d.getSoftInformation(si.data());
+    CHECK(std::signbit(si[0]) && std::signbit(si[7]));
+    // the device batch is not available on a CPU decoder: loud failure
     bool threw = false;
     try {
         d.decodeBatchDevice(nullptr, 1, nullptr);
@@ -66,14 +89,6 @@ int main()
         threw = true;
     }
     CHECK(threw);
-    threw = false;
-    try {
-        float soft[16];
-        d.getSoftCodeword(soft);
-    } catch (const std::logic_error&) {
-        threw = true;
-    }
-    CHECK(threw && d.outputContainer() == nullptr);
     // the GPU factory classifies (and rejects) codes like the reference without a GPU
     threw = false;
     try {

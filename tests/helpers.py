@@ -45,3 +45,18 @@ def node_cover_sets():
     out.append((8, [1, 2, 4]))
     out.append((16, [0, 2, 8]))
     return out
+
+
+def sha256(a):
+    """Digest of an output array as tests/golden/make_digests.py computes it."""
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def reference_digest(name):
+    """The reference's output digests for a full-size GPU test batch
+    (tests/golden/reference_digests.json, made by tests/golden/make_digests.py)."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_digests.json")) as fh:
+        return json.load(fh)["cases"][name]

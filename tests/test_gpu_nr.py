@@ -89,6 +89,19 @@ def test_decode_punctured_matches_oracle(oracle, L):
     assert np.array_equal(d_ok.cpu().numpy(), ook)
     # sanity, not parity: SCL-8 decodes most frames at this SNR, SC some
     assert (gi == info_tx).all(axis=1).mean() > (0.5 if L > 1 else 0.02)
+    if L == 8:
+        # the decoder core against the reference itself (tests/golden/make_digests.py): the
+        # metrics do not depend on the detector; info/ok with the Dummy detector (the
+        # reference has no CRC-11)
+        from helpers import reference_digest, sha256
+        d = reference_digest("config4_nr_scl8")
+        assert sha256(d_met.cpu().numpy()) == d["metrics"]
+        p0 = Plan(1024, 8, fr, systematic=True, crc=0, device=0)
+        d0 = torch.empty((F, 64), dtype=torch.uint8, device="cuda:0")
+        k0 = torch.empty(F, dtype=torch.uint8, device="cuda:0")
+        p0.decode_punctured_device(punc, _t(llr), d0, k0)
+        torch.cuda.synchronize()
+        assert sha256(d0.cpu().numpy()) == d["info"] and sha256(k0.cpu().numpy()) == d["ok"]
 
 
 def test_nr_fixture_core_on_gpu():

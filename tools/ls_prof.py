@@ -2,7 +2,12 @@
 -DPCG_LS_PROF (tools/build_dev_lib.sh ls_prof -DPCG_LS_PROF) selected by PCG_DEV_LIB:
     PCG_DEV_LIB=lib_dev/libpcg_ls_prof.so python tools/ls_prof.py [L [N [F]]]
 Buckets (sclls_kernel.hip, PCG_LS_PROF): op code, +8 for a global-slab source stage,
-+16 for a recomputed (root child) source stage; 60 = extractBestPath + output."""
++16 for a recomputed (root child) source stage, +24 for an LDS source feeding a global
+output; 60 = extractBestPath + output.  Sub-buckets, also counted inside their op's
+bucket: 50 = path selection (ls_select, sort + merge rounds / bitonic merge), 51 = path
+duplication (ls_dup: slot row + codeword prefix copy), 52 = survivor register shuffle
+inside size-8 subtrees (st8_branch), 53 = weak-LLR search of Rate-1 / SPC leaves n >= 8
+(weak_fast, ls_weak on ties)."""
 import ctypes as C
 import os
 import sys
@@ -29,8 +34,10 @@ _native.lib().pcg_dev_opprof_fetch(buf)  # discard the first launch
 p.decode_device(d, di, do)
 torch.cuda.synchronize()
 _native.lib().pcg_dev_opprof_fetch(buf)
-base = {1: "F", 2: "G", 4: "COMB", 40: "R0", 41: "R1", 42: "REP", 43: "SPC", 44: "ST8", 60: "output"}
-cls = {0: "", 8: " (global src)", 16: " (root child)", 24: " (?)"}
+base = {1: "F", 2: "G", 4: "COMB", 40: "R0", 41: "R1", 42: "REP", 43: "SPC", 44: "ST8", 60: "output",
+        50: "  [path selection]", 51: "  [path duplication]", 52: "  [st8 survivor shuffle]",
+        53: "  [weak-LLR search]"}
+cls = {0: "", 8: " (global src)", 16: " (root child)", 24: " (LDS src, global dst)"}
 whole = buf[61]
 print(f"kernel {p.kernel_name()}: {whole:.3e} wave-cycles over {buf[62]} codeword groups")
 rows = []
