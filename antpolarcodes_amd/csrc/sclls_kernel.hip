@@ -1720,6 +1720,9 @@ uint64_t sclls_wave_cap(uint32_t lp, uint32_t wave_lds_floats)
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const uint32_t lds = wave_lds_floats * 4u;
     int res = 0;
+#ifdef PCG_LS_ONLY // dev builds: one instantiation (compile time)
+    res = lp == PCG_LS_ONLY ? ls_resident<PCG_LS_ONLY>(lds) : 0;
+#else
     switch (lp) {
     case 2: res = ls_resident<2>(lds); break;
     case 4: res = ls_resident<4>(lds); break;
@@ -1727,6 +1730,7 @@ uint64_t sclls_wave_cap(uint32_t lp, uint32_t wave_lds_floats)
     case 16: res = ls_resident<16>(lds); break;
     default: res = ls_resident<32>(lds); break;
     }
+#endif
     uint64_t wpc = res > 0 ? (uint64_t)res : 1;
     if (wpc > 8)
         wpc = 8;
@@ -1747,6 +1751,11 @@ int launch_sclls(const KernelArgs& a, hipStream_t stream)
     lds += 64 * sizeof(uint64_t);
 #endif
     const uint32_t lp = a.scl_lp > lp_of(a.L) ? a.scl_lp : lp_of(a.L);
+#ifdef PCG_LS_ONLY
+    if (lp != PCG_LS_ONLY)
+        return -4;
+    hipLaunchKernelGGL(sclls_kernel<PCG_LS_ONLY>, dim3((uint32_t)grid), dim3(64), lds, stream, a);
+#else
     switch (lp) {
     case 2: hipLaunchKernelGGL(sclls_kernel<2>, dim3((uint32_t)grid), dim3(64), lds, stream, a); break;
     case 4: hipLaunchKernelGGL(sclls_kernel<4>, dim3((uint32_t)grid), dim3(64), lds, stream, a); break;
@@ -1755,6 +1764,7 @@ int launch_sclls(const KernelArgs& a, hipStream_t stream)
     case 32: hipLaunchKernelGGL(sclls_kernel<32>, dim3((uint32_t)grid), dim3(64), lds, stream, a); break;
     default: return -4;
     }
+#endif
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

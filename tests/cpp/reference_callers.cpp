@@ -242,6 +242,15 @@ static int run_api()
     return 0;
 }
 
+static void packed_signs(BitContainer* c, size_t N, unsigned char* out)
+{
+    std::vector<float> fb(N);
+    c->getFloatBits(fb.data());
+    std::memset(out, 0, N / 8);
+    for (size_t i = 0; i < N; ++i)
+        out[i / 8] |= (unsigned char)((std::signbit(fb[i]) ? 1u : 0u) << (7 - i % 8));
+}
+
 static int run_gpu(int argc, char** argv)
 {
     CHECK(argc == 5);
@@ -270,9 +279,10 @@ static int run_gpu(int argc, char** argv)
             unsigned char* mDecodedData = mDecoder->packedOutput();
             std::printf("%zu %zu %d ", k, f, success ? 1 : 0);
             hex(mDecodedData, (N - frozen.size()) / 8);
-            // the output container holds the decoded codeword (hard decisions at least)
+            // the output container holds the decoded codeword (its sign bits: getFloatBits; the
+            // reference's getPackedBits is exact for +-0.0 "bits" only, not for a soft codeword)
             std::vector<unsigned char> cw(N / 8);
-            mDecoder->outputContainer()->getPackedBits(cw.data());
+            packed_signs(mDecoder->outputContainer(), N, cw.data());
             std::printf(" ");
             hex(cw.data(), N / 8);
             std::printf("\n");
@@ -284,7 +294,7 @@ static int run_gpu(int argc, char** argv)
     decs[0]->decode();
     decs[0]->getSoftCodeword(soft.data());
     std::vector<unsigned char> cw(N / 8);
-    decs[0]->outputContainer()->getPackedBits(cw.data());
+    packed_signs(decs[0]->outputContainer(), N, cw.data());
     for (size_t i = 0; i < N; ++i)
         CHECK(((cw[i / 8] >> (7 - i % 8)) & 1u) == (std::signbit(soft[i]) ? 1u : 0u));
     bool threw = false;
