@@ -23,6 +23,7 @@ struct pcg_plan {
     uint32_t scl_virt = 0;
     uint32_t scl_fuse = 7;
     uint32_t scl_lp = 0;          // lane-serial SCL: lanes per codeword (0 = list_pow2(L))
+    uint32_t scl_v3 = 0;          // lane-serial SCL: stage 3 recomputed from stage 4 (sclls_layout)
     uint64_t scratch_floats = 0;  // per scratch unit (lane-serial wave)
     float* d_scratch = nullptr;   // grown stream-ordered (hipMallocAsync) when a launch needs more waves
     uint64_t scratch_frames = 0;  // capacity in scratch units
@@ -313,7 +314,8 @@ static int plan_create_impl(pcg_plan** out,
         p->scratch_floats = 0;
         p->wave_lds_floats = pcg::sc_wave_lds_floats(N);
     } else {
-        rc = pcg::sclls_layout(N, L, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats, &p->scl_virt);
+        rc = pcg::sclls_layout(N, L, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats, &p->scl_virt,
+                               &p->scl_v3);
         if (const char* e = getenv("PCG_SCL_FUSE")) {
             p->scl_fuse = (uint32_t)atoi(e);
             p->dev_overrides |= PCG_DEV_SCL_FUSE;
@@ -341,7 +343,7 @@ static int plan_create_impl(pcg_plan** out,
         if (p->dev_flags)
             p->dev_overrides |= PCG_DEV_FLAGS;
     }
-    for (const char* v : {"PCG_SC_KERNEL", "PCG_SCL_LDS_KB", "PCG_SCL_STAGE_LIMIT", "PCG_SCL_VIRT", "PCG_SCL_QUEUE",
+    for (const char* v : {"PCG_SC_KERNEL", "PCG_SCL_V3", "PCG_SCL_LDS_KB", "PCG_SCL_STAGE_LIMIT", "PCG_SCL_VIRT", "PCG_SCL_QUEUE",
                           "PCG_SCQ_WPC", "PCG_SCS_WPC", "PCG_SCL_WPC", "PCG_SCCS_WPC", "PCG_SCLC_WPC",
                           "PCG_SCS_LDS_KB", "PCG_SCS_SL", "PCG_SCCS_LDS_KB", "PCG_SCCS_SL", "PCG_SCLC_LDS_KB",
                           "PCG_SCLC_SL"})
@@ -644,6 +646,7 @@ static int decode_impl(pcg_plan* p,
     a.wave_lds_floats = p->wave_lds_floats;
     a.lds_stage_limit = p->lds_stage_limit;
     a.scl_virt = p->scl_virt;
+    a.scl_v3 = p->scl_v3;
     a.scl_fuse = p->scl_fuse;
     a.scratch_floats = p->scratch_floats;
     a.fmap = fmap;

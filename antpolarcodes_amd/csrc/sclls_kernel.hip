@@ -64,12 +64,18 @@ __host__ __device__ inline uint64_t ls_gl_alpha_floats(uint32_t mt, uint32_t Sl)
     return Sl < mt ? 64ull * ((1ull << mt) - (1ull << Sl)) : 0ull;
 }
 
-__host__ __device__ inline LsLayout ls_layout(uint32_t N, uint32_t Sl)
+// The lowest stages are never stored either (vlow = 1: stage 3, N >= 64; vlow = 2: stages
+// 3 and 4): every reader -- size-8 subtrees, size-8 / size-16 leaves -- recomputes its
+// LLRs from the parent's chunks (F for a left child, G with the left sibling's bits for a
+// right one: V3St, V4St), so the F / G ops writing them vanish and the LDS stages start at
+// 3 + vlow.
+__host__ __device__ inline uint32_t ls_abase(uint32_t vlow) { return 8u << vlow; } // alpha[s] at 64 * (2^s - base)
+__host__ __device__ inline LsLayout ls_layout(uint32_t N, uint32_t Sl, uint32_t vlow)
 {
     LsLayout y;
     uint32_t o = 0;
     y.alpha = o;
-    o += Sl > LS_MINS ? 64u * ((1u << Sl) - 8u) : 0u;
+    o += (1u << Sl) > ls_abase(vlow) ? 64u * ((1u << Sl) - ls_abase(vlow)) : 0u;
     y.bits = o;
     o += 64u * (N >= 32 ? N / 32 : 1u);
     y.total = o;
@@ -87,6 +93,8 @@ struct Ls {
     uint32_t lane, p, gb; // lane, path index in the group, group base lane
     uint32_t share;       // idle lanes help with F/G while P < LP (KernelArgs::scl_fuse bit 1)
     uint32_t stage_root;  // root-child ops stage the channel in LDS (KernelArgs::scl_fuse bit 2)
+    uint32_t vlow;        // stages 3 .. 2+vlow recomputed where read (KernelArgs::scl_v3)
+    uint32_t ab;          // ls_abase(vlow)
     uint64_t ptr;         // slot of stage s at bits 5(s-3)
     float m;              // path metric
 #ifdef PCG_LS_PROF
@@ -119,6 +127,8 @@ struct LdsSt {
     PCG_DEV float4 ld(uint32_t c, uint32_t l) const { return *reinterpret_cast<const float4*>(b + ((c << 6) + l) * 4u); }
     PCG_DEV void st(uint32_t c, const float4& v) const { *reinterpret_cast<float4*>(b + ((c << 6) + lane) * 4u) = v; }
 };
+// (Measured round 3: non-temporal buffer loads / stores for the large slab stages, meant to
+// keep the small ones L2-resident, cost 3-10 % at unchanged traffic -- profiles/r03b_scl8_nt_sweep.txt.)
 struct GlSt {
     float* b;
     uint32_t lane;
@@ -196,7 +206,7 @@ struct Pre<VirtSt> {
 template <int LP>
 PCG_DEV LdsSt lds_st(const Ls<LP>& c, uint32_t s)
 {
-    return LdsSt{ c.lds + c.ly.alpha + 64u * ((1u << s) - 8u), c.lane };
+    return LdsSt{ c.lds + c.ly.alpha + 64u * ((1u << s) - c.ab), c.lane };
 }
 template <int LP>
 PCG_DEV GlSt gl_st(const Ls<LP>& c, uint32_t s)
@@ -204,10 +214,75 @@ PCG_DEV GlSt gl_st(const Ls<LP>& c, uint32_t s)
     return GlSt{ c.gs + 64ull * ((1ull << s) - (1ull << c.Sl)), c.lane };
 }
 
+// Stage 3 of the path, recomputed from its stage-4 chunks (v3): chunk c of the size-8 node
+// at offset o is F(a_c, a_c+2) for a left child, G(a_c, a_c+2, bits o-8+4c ..) for a right
+// one, a = the path's alpha[4] (slot and bit row read through the live context, so a
+// survivor's reload after ls_dup sees the source path's state).
+template <int LP, typename S4>
+struct V3St {
+    const Ls<LP>* cp;
+    S4 s4;
+    uint32_t o; // the size-8 node's offset
+    PCG_DEV float4 ld(uint32_t ch, uint32_t) const
+    {
+        const uint32_t sl = cp->src_lane(4u);
+        const float4 a = s4.ld(ch, sl), b = s4.ld(ch + 2u, sl);
+        if ((o & 8u) == 0u)
+            return f4_f(a, b);
+        const uint32_t i = (o - 8u) + 4u * ch;
+        return f4_g(a, b, cp->row()[(i >> 5) << 6] >> (i & 31u));
+    }
+};
+template <int LP, typename S4>
+struct Pre<V3St<LP, S4>> {
+    static constexpr int U = 2;
+};
+// Stage 4 recomputed from the path's stage-5 chunks (vlow = 2), the same way.
+template <int LP, typename S5>
+struct V4St {
+    const Ls<LP>* cp;
+    S5 s5;
+    uint32_t o; // the size-16 node's offset
+    PCG_DEV float4 ld(uint32_t ch, uint32_t) const
+    {
+        const uint32_t sl = cp->src_lane(5u);
+        const float4 a = s5.ld(ch, sl), b = s5.ld(ch + 4u, sl);
+        if ((o & 16u) == 0u)
+            return f4_f(a, b);
+        const uint32_t i = (o - 16u) + 4u * ch;
+        return f4_g(a, b, cp->row()[(i >> 5) << 6] >> (i & 31u));
+    }
+};
+template <int LP, typename S5>
+struct Pre<V4St<LP, S5>> {
+    static constexpr int U = 2;
+};
+
 // Run fn with the storage of stage s for a node at offset o (wave-uniform choice).
 template <int LP, typename Fn>
 PCG_DEV void with_stage(const Ls<LP>& c, uint32_t s, uint32_t o, Fn&& fn)
 {
+    if (c.vlow >= 2u && s <= 4u) { // stage 4 recomputed from stage 5 (and stage 3 from it)
+        auto go = [&](auto s5) {
+            const V4St<LP, decltype(s5)> v4{ &c, s5, o & ~15u };
+            if (s == 4u)
+                fn(v4);
+            else
+                fn(V3St<LP, decltype(v4)>{ &c, v4, o });
+        };
+        if (5u < c.Sl)
+            go(lds_st(c, 5));
+        else
+            go(gl_st(c, 5));
+        return;
+    }
+    if (c.vlow >= 1u && s == 3u) {
+        if (4u < c.Sl)
+            fn(V3St<LP, LdsSt>{ &c, lds_st(c, 4), o });
+        else
+            fn(V3St<LP, GlSt>{ &c, gl_st(c, 4), o });
+        return;
+    }
     if (s >= c.mt)
         fn(VirtSt{ c.y, c.row(), c.N >> 3, s != c.top, o < (c.N >> 1) });
     else if (s >= c.Sl)
@@ -363,7 +438,7 @@ template <int OPC, int LP>
 PCG_DEV void ls_fg_op(Ls<LP>& c, uint32_t s, uint32_t o, uint32_t P)
 {
     const uint32_t d = s - 1;
-    if (d >= c.mt) // recomputed where it is read
+    if (d >= c.mt || d < 3u + c.vlow) // recomputed where it is read
         return;
     const Share w = ls_share(c, P, s, 1u << (s - 3));
     const uint32_t* row = c.row_of(w.dl);
@@ -517,10 +592,10 @@ PCG_DEV void ls_fgf_root(const Ls<LP>& c, GlSt d1, Dst2 d2, const uint32_t* row,
 template <int LP>
 PCG_DEV uint32_t ls_root_round(const Ls<LP>& c, uint32_t s, uint32_t h)
 {
-    if (!c.stage_root || s != c.mt || s == c.top || s - 2 < c.Sl || c.Sl <= LS_MINS)
+    if (!c.stage_root || s != c.mt || s == c.top || s - 2 < c.Sl || (1u << c.Sl) <= c.ab)
         return 0;
     const uint32_t hq2 = 1u << (s - 4);
-    const uint32_t region = 4u * 64u * ((1u << c.Sl) - 8u); // bytes
+    const uint32_t region = 4u * 64u * ((1u << c.Sl) - c.ab); // bytes
     uint32_t m = hq2;
     while (m > 1 && (64u / LP) * 8u * m * 16u > region)
         m >>= 1;
@@ -889,6 +964,22 @@ PCG_DEV void cx_desc(uint64_t (&k)[8], int a, int b)
     k[b] = sw ? ka : kb;
 }
 
+// The candidate lists come out of r1_spc_cands / st_cands8 almost sorted: with the weak
+// magnitudes ascending (T0 <= T1 <= T2 <= T3, findWeakLlrs' pass order) and fp subtraction
+// monotone in both operands, Rate-1 gives c0 >= c1 >= c2 >= c3 and SPC (either parity)
+// c0 >= c1 >= c2 >= {c3, c4} >= c5 >= c6 >= c7 -- only c3 / c4 are unordered; Repetition's
+// two candidates are.  Among float-equal values the structural order puts the lower
+// candidate index first, which is the key order too (a -0 below a +0 cannot follow from
+// these subtractions), so one compare-exchange of keys sorts every list.
+template <int K>
+PCG_DEV void local_order(uint64_t (&k)[8])
+{
+    if constexpr (K == 2)
+        cx_desc(k, 0, 1);
+    else if constexpr (K == 8)
+        cx_desc(k, 3, 4);
+}
+
 template <int K>
 PCG_DEV void local_sort(uint64_t (&k)[8])
 {
@@ -1055,7 +1146,11 @@ PCG_DEV void ls_select(const Ls<LP>& c, const float (&cv)[8], uint32_t P, uint32
         const uint32_t o = (act && j < K) ? ord_of(cv[j]) : 0u;
         k[j] = ((uint64_t)o << 32) | (~code);
     }
+#ifdef PCG_LS_FULL_LOCAL_SORT // dev: the general 19-comparator network
     local_sort<K>(k);
+#else
+    local_order<K>(k);
+#endif
     const uint32_t R = C > np ? np + 1 : C;
     float prev = 0.0f;
     bool tie = false;
@@ -1505,7 +1600,9 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
     c.top = a.log2N;
     c.Sl = a.lds_stage_limit;
     c.mt = ls_mtop(c.top, a.scl_virt);
-    c.ly = ls_layout(a.N, a.lds_stage_limit);
+    c.vlow = a.scl_v3;
+    c.ab = ls_abase(c.vlow);
+    c.ly = ls_layout(a.N, a.lds_stage_limit, c.vlow);
     c.lane = threadIdx.x;
     c.share = (a.scl_fuse >> 1) & 1u;
     c.stage_root = (a.scl_fuse >> 2) & 1u;
@@ -1657,14 +1754,21 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
 } // namespace
 
 int sclls_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* lds_stage_limit,
-                 uint64_t* scratch_floats, uint32_t* virt)
+                 uint64_t* scratch_floats, uint32_t* virt, uint32_t* v3)
 {
     if (L < 2 || L > 32 || N < 8)
         return -4;
     const uint32_t top = (uint32_t)__builtin_ctz(N);
     if (top > 3 + 12) // 5-bit slot fields for stages 3 .. top-1 in 64 bits
         return -4;
-    uint32_t budget = 24 * 1024 / 4; // floats per wave (measured best at N = 1024, L = 8: S_l = 6, 7 waves/CU)
+    // stage 3 recomputed from stored stage-4 chunks (N >= 64); PCG_SCL_V3 = 0 stores it,
+    // 2 also recomputes stage 4 from stage 5 (N >= 128)
+    uint32_t w3 = top >= 6 ? 1u : 0u;
+    if (const char* e = getenv("PCG_SCL_V3")) {
+        const uint32_t v = (uint32_t)atoi(e);
+        w3 = v == 0 ? 0u : (v >= 2 && top >= 7 ? 2u : w3);
+    }
+    uint32_t budget = 24 * 1024 / 4; // floats per wave (N = 1024, L = 8: S_l = 6, stages 4-5 in LDS: 20 KB, 8 waves/CU)
     const uint32_t bitsf = 64u * (N >= 32 ? N / 32 : 1u);
     if (bitsf + 2048u > budget) // large N: the bit rows alone fill 24 KB; keep stages 3-4 on chip
         budget = bitsf + 2048u;  // (N = 4096: 40 KB, 4 waves/CU: +3 % over 24 KB, r02y sweep)
@@ -1677,20 +1781,21 @@ int sclls_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* ld
     }
     const uint32_t mt = ls_mtop(top, vt);
     uint32_t Sl = mt;
-    while (Sl > LS_MINS && ls_layout(N, Sl).total > budget)
+    while (Sl > LS_MINS && ls_layout(N, Sl, w3).total > budget)
         --Sl;
     if (const char* e = getenv("PCG_SCL_STAGE_LIMIT")) {
         const uint32_t v = (uint32_t)atoi(e);
         if (v >= LS_MINS && v <= mt)
             Sl = v;
     }
-    const LsLayout ly = ls_layout(N, Sl);
+    const LsLayout ly = ls_layout(N, Sl, w3);
     if (ly.total * 4 > 160 * 1024)
         return -4;
     *wave_lds_floats = ly.total;
     *lds_stage_limit = Sl;
     *scratch_floats = ls_gl_alpha_floats(mt, Sl) + 1024;
     *virt = vt;
+    *v3 = w3;
     return 0;
 }
 

@@ -378,7 +378,9 @@ def main(argv=None):
         traffic, traffic_note = None, None
         if measure and rank == 0:
             probe = Plan(N, L, frozen, systematic=True, crc=crc, device=-1, adaptive=adaptive, fixed=fixed)
-            traffic, traffic_note = measure_traffic(args, probe.kernel_name() if not adaptive else None, F)
+            # adaptive plans: the list stage's kernel (the dominant one, r02af stats: 61 % of the
+            # step) -- its FETCH/WRITE per launch, over the CRC failures it decodes
+            traffic, traffic_note = measure_traffic(args, probe.kernel_name(), F)
             probe.close()
         torch.cuda.set_device(local)
         dev = torch.device(f"cuda:{local}")
@@ -488,7 +490,7 @@ def main(argv=None):
         else:
             line["frame_error_rate"] = fer
             line["crc_ok_rate"] = ok_rate
-            if traffic is None and not adaptive:
+            if traffic is None:
                 traffic, why = stamped_traffic(args.mode, kernel, digest)
                 traffic_note = traffic_note or why
                 if traffic is not None:
@@ -502,9 +504,11 @@ def main(argv=None):
                     roof["traffic_write_bytes_per_codeword"] = traffic["write_bytes_per_launch"] / F
                 roof["traffic_frac"] = tb / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if kern_ms > 0 else None
                 roof["traffic_source"] = traffic["source"]
+                if adaptive:
+                    roof["traffic_scope"] = (f"{kernel}: the list stage over the frames whose Fast-SSC CRC check "
+                                             f"failed; the Fast-SSC stage is another kernel")
             else:
-                roof["traffic_note"] = traffic_note or ("adaptive: several kernels per step" if adaptive else
-                                                        "not measured")
+                roof["traffic_note"] = traffic_note or "not measured"
             if world == 1 and not args.no_copy_bw:
                 roof["measured_copy_GBps"] = copy_bandwidth(torch, dev)
                 roof["frac_of_measured_copy"] = achieved / roof["measured_copy_GBps"]
