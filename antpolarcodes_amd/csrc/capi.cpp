@@ -24,6 +24,7 @@ struct pcg_plan {
     uint32_t scl_fuse = 7;
     uint32_t scl_lp = 0;          // lane-serial SCL: lanes per codeword (0 = list_pow2(L))
     uint32_t scl_v3 = 0;          // lane-serial SCL: stage 3 recomputed from stage 4 (sclls_layout)
+    uint32_t scl_sb = 0;          // lane-serial SCL: bit buffers below this stage in LDS (0: codeword rows)
     uint64_t scratch_floats = 0;  // per scratch unit (lane-serial wave)
     float* d_scratch = nullptr;   // grown stream-ordered (hipMallocAsync) when a launch needs more waves
     uint64_t scratch_frames = 0;  // capacity in scratch units
@@ -314,12 +315,6 @@ static int plan_create_impl(pcg_plan** out,
         p->scratch_floats = 0;
         p->wave_lds_floats = pcg::sc_wave_lds_floats(N);
     } else {
-        rc = pcg::sclls_layout(N, L, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats, &p->scl_virt,
-                               &p->scl_v3);
-        if (const char* e = getenv("PCG_SCL_FUSE")) {
-            p->scl_fuse = (uint32_t)atoi(e);
-            p->dev_overrides |= PCG_DEV_SCL_FUSE;
-        }
         // lanes per codeword: the caller's request, else the PCG_SCL_LP dev override; used
         // when it is a power of two between list_pow2(L) and 32
         if (const char* e = getenv("PCG_SCL_LP"); e && scl_lp == 0) {
@@ -329,6 +324,12 @@ static int plan_create_impl(pcg_plan** out,
         p->scl_lp = list_pow2(L);
         if (scl_lp > p->scl_lp && scl_lp <= 32 && (scl_lp & (scl_lp - 1)) == 0)
             p->scl_lp = scl_lp;
+        rc = pcg::sclls_layout(N, L, p->scl_lp, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats,
+                               &p->scl_virt, &p->scl_v3, &p->scl_sb);
+        if (const char* e = getenv("PCG_SCL_FUSE")) {
+            p->scl_fuse = (uint32_t)atoi(e);
+            p->dev_overrides |= PCG_DEV_SCL_FUSE;
+        }
         if (rc != 0) {
             delete p;
             return fail(rc, "list decoding layout unsupported for this N/L");
@@ -647,6 +648,7 @@ static int decode_impl(pcg_plan* p,
     a.lds_stage_limit = p->lds_stage_limit;
     a.scl_virt = p->scl_virt;
     a.scl_v3 = p->scl_v3;
+    a.scl_sb = p->scl_sb;
     a.scl_fuse = p->scl_fuse;
     a.scratch_floats = p->scratch_floats;
     a.fmap = fmap;

@@ -54,6 +54,9 @@ struct KernelArgs {
     uint32_t scl_lp;
     // lane-serial SCL: stages 3 .. 2+scl_v3 are recomputed wherever they are read (sclls_layout)
     uint32_t scl_v3;
+    // lane-serial SCL with lazy bit buffers (LP >= PCG_LS_DBITS_LP): D[4 .. scl_sb-1] in LDS,
+    // the rest in the global slab; 0 for the per-lane codeword rows of smaller LP
+    uint32_t scl_sb;
 };
 
 // PCG_*_WPC developer overrides of the waves per CU: ignored unless a positive number
@@ -99,8 +102,8 @@ inline uint64_t wave_units(uint64_t F, uint32_t frames_per_wave, uint64_t cap)
     return need < cap ? need : cap;
 }
 // lane-serial SCL kernel (sclls_kernel.hip), 64 / L' codewords per wave
-int sclls_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* lds_stage_limit,
-                 uint64_t* scratch_floats, uint32_t* virt, uint32_t* v3);
+int sclls_layout(uint32_t N, uint32_t L, uint32_t lp, uint32_t* wave_lds_floats, uint32_t* lds_stage_limit,
+                 uint64_t* scratch_floats, uint32_t* virt, uint32_t* v3, uint32_t* sb);
 uint64_t sclls_wave_cap(uint32_t lp, uint32_t wave_lds_floats);
 int launch_sclls(const KernelArgs& a, hipStream_t stream);
 // 8-bit SCL (scl_char_kernel.hip): LDS dwords per wave, LDS stage limit, global scratch dwords

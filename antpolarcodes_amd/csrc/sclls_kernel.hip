@@ -21,7 +21,15 @@
 //     ones are dead then) in its own lane; a branching leaf copies the table row of
 //     the path each survivor descends from -- the reference's lazy DataPool copy
 //     (scl_avx_float.cpp:21-171) without moving any LLRs;
-//   * the packed codeword bits of the path, one LDS word column per lane.
+//   * the path's bits.  LP < PCG_LS_DBITS_LP: the packed codeword, one LDS word column
+//     per lane; a survivor of a branching leaf copies the prefix decoded so far from the
+//     path it descends from.  LP >= PCG_LS_DBITS_LP (N = 4096 rows would fill the LDS):
+//     lazily copied like the LLRs -- D[s] (2^s bits, stages 4 .. top) holds the two
+//     decoded children of the current stage-s node, left half then right half; a child
+//     (leaf or Combine) writes its half in the path's own lane, copying the left half
+//     over from its slot when it writes the right one, and its own slot table bptr.
+//     D[top] ends as the codeword.  Survivors copy ptr and bptr only: no bits move (D
+//     stages < Sb in LDS, the rest in the global slab).
 // Path selection (simplePartialSortDescending, arrayfuncs.h:161-183) is a merge of
 // the LP lanes' locally sorted candidate lists; exact ties (the only case where the
 // reference's swap order is observable) switch the wave to a literal simulation.
@@ -38,10 +46,23 @@ namespace {
 
 constexpr uint32_t LS_MINS = 3; // lowest memory stage: size-8 nodes
 
+// Lanes per codeword from which the bits are lazy D buffers instead of codeword rows
+// (measured round 3: SCL-32 N = 4096 6.6e5 -> 8.6e5 cw/s from 4 to 8 waves/CU; SCL-8
+// N = 1024 2.22e7 -> 2.01e7, its Combines and G bit reads cost more than the row copies)
+#ifndef PCG_LS_DBITS_LP
+#define PCG_LS_DBITS_LP 16
+#endif
+
+// Bit words through address-space qualified pointers: an LDS and a global read behind one
+// wave-uniform branch must stay two instructions (ds_read / global_load), never one flat
+// load (whose wait would also drain the op's in-flight slab loads).
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(1))) uint32_t gl_u32;
+
 // ---- layout --------------------------------------------------------------------------
 struct LsLayout {
-    uint32_t alpha; // 64 * (2^Sl - 8) floats (stages [3, Sl))
-    uint32_t bits;  // 64 * W words
+    uint32_t alpha; // 64 * (2^Sl - 2^(3+vlow)) floats (stages [3+vlow, Sl))
+    uint32_t d;     // 64 * 2^(Sb-5) words: D stages [4, Sb)
     uint32_t total;
 };
 
@@ -70,14 +91,30 @@ __host__ __device__ inline uint64_t ls_gl_alpha_floats(uint32_t mt, uint32_t Sl)
 // right one: V3St, V4St), so the F / G ops writing them vanish and the LDS stages start at
 // 3 + vlow.
 __host__ __device__ inline uint32_t ls_abase(uint32_t vlow) { return 8u << vlow; } // alpha[s] at 64 * (2^s - base)
-__host__ __device__ inline LsLayout ls_layout(uint32_t N, uint32_t Sl, uint32_t vlow)
+
+// D buffers: D[s] at word ls_doff(s) of the lane's column (D[4], D[5]: one word each, D[s]
+// 2^(s-5) words at 2^(s-5); the N = 8 code's D[3] is D[4]'s word).  Stages [4, Sb) in
+// LDS, [Sb, top] in the global slab (Sb >= 5).
+__host__ __device__ inline uint32_t ls_doff(uint32_t s) { return s <= 4u ? 0u : 1u << (s - 5u); }
+__host__ __device__ inline uint32_t ls_dlds_words(uint32_t top, uint32_t Sb)
+{
+    if (Sb == 0) // codeword rows: N bits per lane
+        return top >= 5u ? 1u << (top - 5u) : 1u;
+    const uint32_t e = Sb < top + 1u ? Sb : top + 1u;
+    return e <= 5u ? 1u : 1u << (e - 5u);
+}
+__host__ __device__ inline uint32_t ls_dgl_words(uint32_t top, uint32_t Sb)
+{
+    return Sb != 0 && Sb <= top ? (1u << (top - 4u)) - (1u << (Sb - 5u)) : 0u;
+}
+__host__ __device__ inline LsLayout ls_layout(uint32_t top, uint32_t Sl, uint32_t vlow, uint32_t Sb)
 {
     LsLayout y;
     uint32_t o = 0;
     y.alpha = o;
     o += (1u << Sl) > ls_abase(vlow) ? 64u * ((1u << Sl) - ls_abase(vlow)) : 0u;
-    y.bits = o;
-    o += 64u * (N >= 32 ? N / 32 : 1u);
+    y.d = o;
+    o += 64u * ls_dlds_words(top, Sb);
     y.total = o;
     return y;
 }
@@ -85,6 +122,7 @@ __host__ __device__ inline LsLayout ls_layout(uint32_t N, uint32_t Sl, uint32_t 
 // ---- per-wave context ----------------------------------------------------------------
 template <int LP>
 struct Ls {
+    static constexpr bool DB = LP >= PCG_LS_DBITS_LP; // lazy D buffers, else codeword rows
     float* lds;
     float* gs;        // this wave's global scratch slab
     const float* y;   // this lane's codeword channel LLRs
@@ -95,7 +133,12 @@ struct Ls {
     uint32_t stage_root;  // root-child ops stage the channel in LDS (KernelArgs::scl_fuse bit 2)
     uint32_t vlow;        // stages 3 .. 2+vlow recomputed where read (KernelArgs::scl_v3)
     uint32_t ab;          // ls_abase(vlow)
+    uint32_t Sb;          // D stages [4, Sb) in LDS (KernelArgs::scl_sb)
+    lds_u32* dl;          // LDS D region: word w of lane l at [(w << 6) + l]
+    gl_u32* dg;           // this wave's global D region (stages >= Sb)
     uint64_t ptr;         // slot of stage s at bits 5(s-3)
+    uint64_t bptr;        // D slot of stage s at bits 5(max(s,4)-4)
+    bool fin;             // the root's Combine left the codeword in the LDS stage region
     float m;              // path metric
 #ifdef PCG_LS_PROF
     uint64_t* lprof;
@@ -116,9 +159,74 @@ struct Ls {
         const uint32_t sh = 5u * (s - LS_MINS);
         ptr = (ptr & ~(31ull << sh)) | ((uint64_t)p << sh);
     }
-    PCG_DEV uint32_t* row() const { return reinterpret_cast<uint32_t*>(lds + ly.bits) + lane; } // word w at [w*64]
-    PCG_DEV uint32_t* row_of(uint32_t l) const { return reinterpret_cast<uint32_t*>(lds + ly.bits) + l; }
+    PCG_DEV lds_u32* row() const { return dl + lane; } // codeword rows: word w at [w*64]
+    PCG_DEV lds_u32* row_of(uint32_t l) const { return dl + l; }
+    PCG_DEV static uint32_t bfield(uint32_t s) { return 5u * ((s > 4u ? s : 4u) - 4u); }
+    PCG_DEV uint32_t dslot(uint32_t s) const { return (uint32_t)((bptr >> bfield(s)) & 31u); }
+    PCG_DEV uint32_t dlane(uint32_t s) const { return gb | dslot(s); }
+    PCG_DEV void down(uint32_t s) { // D[s] of this path is now in its own lane
+        const uint32_t sh = bfield(s);
+        bptr = (bptr & ~(31ull << sh)) | ((uint64_t)p << sh);
+    }
+    // word w of D[s] in lane l / store into the own lane (wave-uniform storage choice)
+    PCG_DEV uint32_t dld(uint32_t s, uint32_t w, uint32_t l) const
+    {
+        const uint32_t o = ls_doff(s) + w;
+        if (s < Sb)
+            return dl[(o << 6) + l];
+        return dg[((uint64_t)(o - (1u << (Sb - 5u))) << 6) + l];
+    }
+    PCG_DEV void dst(uint32_t s, uint32_t w, uint32_t v) const
+    {
+        const uint32_t o = ls_doff(s) + w;
+        if (s < Sb)
+            dl[(o << 6) + lane] = v;
+        else
+            dg[((uint64_t)(o - (1u << (Sb - 5u))) << 6) + lane] = v;
+    }
 };
+
+// The bits of D[s] of one path, read a word at a time by G ops and recomputed right
+// children (wave-uniform LDS / global choice per read).
+// (Codeword rows: the row of the path's lane, relative positions from the node's offset.)
+struct DBits {
+    const lds_u32* l; // LDS words of D[s] (stage < Sb) or the codeword rows
+    const gl_u32* g;  // global words (stage >= Sb)
+    uint32_t lane;
+    bool glob;
+    uint32_t base; // position of relative bit 0 (rows: the node's offset)
+    PCG_DEV uint32_t word(uint32_t w) const { return glob ? g[((uint64_t)w << 6) + lane] : l[(w << 6) + lane]; }
+    // bits from relative position i (the 32 - (i & 31) bits of its word); the word holding it
+    PCG_DEV uint32_t at(uint32_t i) const { return word((base + i) >> 5) >> ((base + i) & 31u); }
+    PCG_DEV uint32_t wat(uint32_t i) const { return word((base + i) >> 5); }
+};
+template <int LP>
+PCG_DEV DBits dbits(const Ls<LP>& c, uint32_t s, uint32_t lane)
+{
+    DBits b;
+    const uint32_t o = ls_doff(s);
+    b.glob = s >= c.Sb;
+    b.l = c.dl + (o << 6);
+    b.g = c.dg + ((uint64_t)(b.glob ? o - (1u << (c.Sb - 5u)) : 0u) << 6);
+    b.lane = lane;
+    b.base = 0;
+    return b;
+}
+template <int LP>
+PCG_DEV DBits rowbits(const Ls<LP>& c, uint32_t lane, uint32_t base)
+{
+    return DBits{ c.dl, nullptr, lane, false, base };
+}
+// the bits a G of the stage-s node at o reads (its left child's) for the path in lane dl
+// (D: the path's D[s] slot lane bl)
+template <int LP>
+PCG_DEV DBits gbits(const Ls<LP>& c, uint32_t s, uint32_t o, uint32_t dl, uint32_t bl)
+{
+    if constexpr (Ls<LP>::DB)
+        return dbits(c, s, bl);
+    else
+        return rowbits(c, dl, o);
+}
 
 // Stage storages.  ld(c, l): float4 chunk c of lane l's buffer; st(c, v): own lane.
 struct LdsSt {
@@ -162,30 +270,36 @@ struct ChSt { // the channel LLRs of the lane's own codeword (stage top)
 template <bool LEFT>
 struct RootSt { // stage top-1, left or right child of the root
     const float* y;
-    const uint32_t* row; // the lane's bit row (word w at [w*64])
-    uint32_t hq1;        // N/8 chunks: distance of y_j+N/2
+    DBits lb;     // the path's D[top]: the left child's bits (right child only)
+    uint32_t hq1; // N/8 chunks: distance of y_j+N/2
     PCG_DEV float4 ld(uint32_t c, uint32_t) const
     {
         const float4 a = chan_ld(y, c);
         const float4 b = chan_ld(y, c + hq1);
         if (LEFT)
             return f4_f(a, b);
-        const uint32_t i = 4u * c;
-        return f4_g(a, b, row[(i >> 5) << 6] >> (i & 31u));
+        return f4_g(a, b, lb.at(4u * c));
     }
 };
 // Any recomputed stage behind one wave-uniform switch (leaves and size-8 subtrees at
 // stage top or top-1: rare, so one instantiation serves all of them).
+// (The left bits are read through the live context: a survivor's reload after ls_dup
+// sees the source path's D[top].)
+template <int LP>
 struct VirtSt {
-    const float* y;
-    const uint32_t* row;
+    const Ls<LP>* cp;
     uint32_t hq1;
     bool root, left;
     PCG_DEV float4 ld(uint32_t c, uint32_t l) const
     {
         if (!root)
-            return ChSt{ y }.ld(c, l);
-        return left ? RootSt<true>{ y, row, hq1 }.ld(c, l) : RootSt<false>{ y, row, hq1 }.ld(c, l);
+            return ChSt{ cp->y }.ld(c, l);
+        if (left)
+            return RootSt<true>{ cp->y, DBits{}, hq1 }.ld(c, l);
+        if constexpr (Ls<LP>::DB)
+            return RootSt<false>{ cp->y, dbits(*cp, cp->top, cp->dlane(cp->top)), hq1 }.ld(c, l);
+        else
+            return RootSt<false>{ cp->y, rowbits(*cp, cp->lane, 0u), hq1 }.ld(c, l);
     }
 };
 
@@ -198,8 +312,8 @@ template <bool LEFT>
 struct Pre<RootSt<LEFT>> {
     static constexpr int U = 2;
 };
-template <>
-struct Pre<VirtSt> {
+template <int LP>
+struct Pre<VirtSt<LP>> {
     static constexpr int U = 2;
 };
 
@@ -229,6 +343,9 @@ struct V3St {
         const float4 a = s4.ld(ch, sl), b = s4.ld(ch + 2u, sl);
         if ((o & 8u) == 0u)
             return f4_f(a, b);
+        // the left sibling's 8 bits: D[4] bits 0..7, or the row's o-8 ..
+        if constexpr (Ls<LP>::DB)
+            return f4_g(a, b, cp->dld(4u, 0u, cp->dlane(4u)) >> (4u * ch));
         const uint32_t i = (o - 8u) + 4u * ch;
         return f4_g(a, b, cp->row()[(i >> 5) << 6] >> (i & 31u));
     }
@@ -249,6 +366,9 @@ struct V4St {
         const float4 a = s5.ld(ch, sl), b = s5.ld(ch + 4u, sl);
         if ((o & 16u) == 0u)
             return f4_f(a, b);
+        // the left sibling's 16 bits: D[5] bits 0..15, or the row's o-16 ..
+        if constexpr (Ls<LP>::DB)
+            return f4_g(a, b, cp->dld(5u, 0u, cp->dlane(5u)) >> (4u * ch));
         const uint32_t i = (o - 16u) + 4u * ch;
         return f4_g(a, b, cp->row()[(i >> 5) << 6] >> (i & 31u));
     }
@@ -284,7 +404,7 @@ PCG_DEV void with_stage(const Ls<LP>& c, uint32_t s, uint32_t o, Fn&& fn)
         return;
     }
     if (s >= c.mt)
-        fn(VirtSt{ c.y, c.row(), c.N >> 3, s != c.top, o < (c.N >> 1) });
+        fn(VirtSt<LP>{ &c, c.N >> 3, s != c.top, o < (c.N >> 1) });
     else if (s >= c.Sl)
         fn(gl_st(c, s));
     else
@@ -344,7 +464,16 @@ struct Share {
     uint32_t h, i; // lanes per path, this lane's index among them
     bool act;
     uint32_t sl;   // lane holding the source stage of the path
+    uint32_t bl;   // lane holding the path's D[s] (a G's left bits)
+    bool shr;      // lanes work on other paths (wave-uniform)
 };
+// lane holding D[s] of the path in lane dl
+template <int LP>
+PCG_DEV uint32_t path_dlane(const Ls<LP>& c, uint32_t dl, uint32_t s)
+{
+    const uint32_t lo = shfl((uint32_t)c.bptr, (int)dl), hi = shfl((uint32_t)(c.bptr >> 32), (int)dl);
+    return c.gb | (uint32_t)(((((uint64_t)hi << 32) | lo) >> Ls<LP>::bfield(s)) & 31u);
+}
 template <int LP>
 PCG_DEV Share ls_share(const Ls<LP>& c, uint32_t P, uint32_t s, uint32_t nch)
 {
@@ -355,6 +484,8 @@ PCG_DEV Share ls_share(const Ls<LP>& c, uint32_t P, uint32_t s, uint32_t nch)
         w.i = 0;
         w.act = c.p < P;
         w.sl = c.src_lane(s < c.mt ? s : LS_MINS);
+        w.bl = Ls<LP>::DB ? c.dlane(s) : 0u;
+        w.shr = false;
         return w;
     }
     uint32_t pp = 1;
@@ -371,7 +502,18 @@ PCG_DEV Share ls_share(const Ls<LP>& c, uint32_t P, uint32_t s, uint32_t nch)
     const uint32_t lo = shfl((uint32_t)c.ptr, (int)w.dl), hi = shfl((uint32_t)(c.ptr >> 32), (int)w.dl);
     const uint64_t ptr = ((uint64_t)hi << 32) | lo;
     w.sl = c.gb | (uint32_t)((ptr >> (5u * (s - LS_MINS))) & 31u); // stages >= mt: unused
+    w.bl = Ls<LP>::DB ? path_dlane(c, w.dl, s) : 0u;
+    w.shr = true;
     return w;
+}
+// the root's left-child bits of a recomputed right child (D[top], or the row) of path w.dl
+template <int LP>
+PCG_DEV DBits root_bits(const Ls<LP>& c, const Share& w)
+{
+    if constexpr (Ls<LP>::DB)
+        return dbits(c, c.top, w.shr ? path_dlane(c, w.dl, c.top) : c.dlane(c.top));
+    else
+        return rowbits(c, w.dl, 0u);
 }
 template <typename S>
 struct Off { // chunks [b, ...) of a storage
@@ -388,7 +530,7 @@ struct Pre<Off<S>> {
 // h = 2^(s-1) >= 8 elements = hq float4 chunks (a power of two >= 2); the two halves
 // are streamed together, chunks [cb, cb+n) by this lane.
 template <int OPC, int LP, typename Src, typename Dst>
-PCG_DEV void ls_fg(Src src, Dst dst, const uint32_t* row, uint32_t s, uint32_t o, const Share& w)
+PCG_DEV void ls_fg(Src src, Dst dst, const DBits& lb, uint32_t s, const Share& w)
 {
     constexpr int U = Pre<Src>::U;
     const uint32_t hq = 1u << (s - 3), n = hq / w.h, cb = n * w.i;
@@ -398,10 +540,8 @@ PCG_DEV void ls_fg(Src src, Dst dst, const uint32_t* row, uint32_t s, uint32_t o
     const Off<Src> sa{ src, cb }, sb{ src, hq + cb };
     auto body = [&](const float4 (&xa)[U], const float4 (&xb)[U], uint32_t c0, uint32_t valid) {
         uint32_t wb = 0;
-        if (OPC == OP_G) {
-            const uint32_t i = o + 4u * (cb + c0); // the batch's 4U <= 16 elements share a bit word
-            wb = row[(i >> 5) << 6] >> (i & 31u);
-        }
+        if (OPC == OP_G) // the batch's 4U <= 16 elements share a bit word
+            wb = lb.at(4u * (cb + c0));
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if ((uint32_t)u < valid) {
@@ -441,19 +581,19 @@ PCG_DEV void ls_fg_op(Ls<LP>& c, uint32_t s, uint32_t o, uint32_t P)
     if (d >= c.mt || d < 3u + c.vlow) // recomputed where it is read
         return;
     const Share w = ls_share(c, P, s, 1u << (s - 3));
-    const uint32_t* row = c.row_of(w.dl);
+    const DBits lb = gbits(c, s, o, w.dl, w.bl);
     auto run = [&](auto dst) {
         dst.lane = w.dl;
         if (s == c.top)
-            ls_fg<OPC, LP>(ChSt{ c.y }, dst, row, s, o, w);
+            ls_fg<OPC, LP>(ChSt{ c.y }, dst, lb, s, w);
         else if (s >= c.mt && o < (c.N >> 1))
-            ls_fg<OPC, LP>(RootSt<true>{ c.y, row, c.N >> 3 }, dst, row, s, o, w);
+            ls_fg<OPC, LP>(RootSt<true>{ c.y, DBits{}, c.N >> 3 }, dst, lb, s, w);
         else if (s >= c.mt)
-            ls_fg<OPC, LP>(RootSt<false>{ c.y, row, c.N >> 3 }, dst, row, s, o, w);
+            ls_fg<OPC, LP>(RootSt<false>{ c.y, root_bits(c, w), c.N >> 3 }, dst, lb, s, w);
         else if (s >= c.Sl)
-            ls_fg<OPC, LP>(gl_st(c, s), dst, row, s, o, w);
+            ls_fg<OPC, LP>(gl_st(c, s), dst, lb, s, w);
         else
-            ls_fg<OPC, LP>(lds_st(c, s), dst, row, s, o, w);
+            ls_fg<OPC, LP>(lds_st(c, s), dst, lb, s, w);
     };
     if (d >= c.Sl)
         run(gl_st(c, d));
@@ -471,7 +611,7 @@ PCG_DEV void ls_fg_op(Ls<LP>& c, uint32_t s, uint32_t o, uint32_t P)
 #define PCG_FGF_U 1 // batch depth of the fused op (VGPR pressure: 2 spills 31 more registers)
 #endif
 template <int OPC, int LP, typename Src, typename Dst1, typename Dst2>
-PCG_DEV void ls_fgf(Src src, Dst1 d1, Dst2 d2, const uint32_t* row, uint32_t s, uint32_t o, const Share& w)
+PCG_DEV void ls_fgf(Src src, Dst1 d1, Dst2 d2, const DBits& lb, uint32_t s, const Share& w)
 {
     constexpr int U = Pre<Src>::U >= 4 ? PCG_FGF_U : 1; // four source chunks per output chunk
     const uint32_t hq = 1u << (s - 3), hq2 = hq >> 1, n = hq2 / w.h, cb = n * w.i;
@@ -490,9 +630,9 @@ PCG_DEV void ls_fgf(Src src, Dst1 d1, Dst2 d2, const uint32_t* row, uint32_t s, 
     auto body = [&](const float4 (&x)[4][U], uint32_t c0) {
         uint32_t wa = 0, wb = 0;
         if (OPC == OP_G) { // 4U <= 8 elements from an 8-aligned start share a bit word
-            const uint32_t ia = o + 4u * (cb + c0), ib = ia + 4u * hq2;
-            wa = row[(ia >> 5) << 6] >> (ia & 31u);
-            wb = row[(ib >> 5) << 6] >> (ib & 31u);
+            const uint32_t ia = 4u * (cb + c0), ib = ia + 4u * hq2;
+            wa = lb.at(ia);
+            wb = lb.at(ib);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -527,7 +667,7 @@ PCG_DEV void ls_fgf(Src src, Dst1 d1, Dst2 d2, const uint32_t* row, uint32_t s, 
 // the channel chunks a_k (alpha[s] chunks c2, c2+hq, c2+hq2, c2+hq2+hq), k >= 4 the
 // chunks a_k + N/8 (their partners y_j+N/2).
 template <int OPC, bool LEFT, int LP, typename Dst2>
-PCG_DEV void ls_fgf_root(const Ls<LP>& c, GlSt d1, Dst2 d2, const uint32_t* row, uint32_t s, uint32_t o,
+PCG_DEV void ls_fgf_root(const Ls<LP>& c, GlSt d1, Dst2 d2, const DBits& lb, const DBits& rb, uint32_t s,
                          const Share& w, uint32_t m)
 {
     const uint32_t hq = 1u << (s - 3), hq2 = hq >> 1, hq1 = c.N >> 3;
@@ -537,6 +677,22 @@ PCG_DEV void ls_fgf_root(const Ls<LP>& c, GlSt d1, Dst2 d2, const uint32_t* row,
     const uint32_t n = m / w.h;                 // output chunks per lane per round
     const uint64_t yp = (uint64_t)(uintptr_t)c.y;
     const float4* mine = reinterpret_cast<const float4*>(stg) + (c.lane / LP) * per;
+    // s >= 7: the bits of 8 aligned output chunks are one word per source (the root's left
+    // half for a right child, the op's own G bits), loaded per 8 chunks -- the first ones
+    // while the DMA runs
+    const bool grp = hq2 >= 8u;
+    uint32_t rw[4] = { 0, 0, 0, 0 }, lw[2] = { 0, 0 };
+    auto words = [&](uint32_t cg) {
+        if (!LEFT) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                rw[k] = rb.wat(4u * (cg + ((k & 1) ? hq : 0u) + ((k & 2) ? hq2 : 0u)));
+        }
+        if (OPC == OP_G) { // (a row's node offset is a multiple of 32 here)
+            lw[0] = lb.wat(4u * cg);
+            lw[1] = lb.wat(4u * (cg + hq2));
+        }
+    };
     for (uint32_t r = 0; r < hq2; r += m) {
         __builtin_amdgcn_s_waitcnt(0); // the previous round's LDS reads have completed
         __builtin_amdgcn_wave_barrier();
@@ -550,12 +706,17 @@ PCG_DEV void ls_fgf_root(const Ls<LP>& c, GlSt d1, Dst2 d2, const uint32_t* row,
             const float* src = reinterpret_cast<const float*>((uintptr_t)(((uint64_t)hi << 32) | lo)) + 4u * a;
             __builtin_amdgcn_global_load_lds(src, stg + t * 256u, 16, 0, 0);
         }
+        if (grp && w.act)
+            words(r + w.i * n);
         __builtin_amdgcn_s_waitcnt(0);
         __builtin_amdgcn_wave_barrier();
         if (!w.act)
             continue;
         for (uint32_t uu = 0; uu < n; ++uu) {
             const uint32_t u = w.i * n + uu, c2 = r + u;
+            if (grp && uu > 0 && (uu & 7u) == 0)
+                words(c2);
+            const uint32_t gs = 4u * (c2 & 7u);
             float4 yv[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k)
@@ -566,15 +727,15 @@ PCG_DEV void ls_fgf_root(const Ls<LP>& c, GlSt d1, Dst2 d2, const uint32_t* row,
                 if (LEFT) {
                     x[k] = f4_f(yv[k], yv[k + 4]);
                 } else {
-                    const uint32_t a = c2 + ((k & 1) ? hq : 0u) + ((k & 2) ? hq2 : 0u), i = 4u * a;
-                    x[k] = f4_g(yv[k], yv[k + 4], row[(i >> 5) << 6] >> (i & 31u));
+                    const uint32_t a = c2 + ((k & 1) ? hq : 0u) + ((k & 2) ? hq2 : 0u);
+                    x[k] = f4_g(yv[k], yv[k + 4], grp ? rw[k] >> gs : rb.at(4u * a));
                 }
             }
             uint32_t wa = 0, wb = 0;
             if (OPC == OP_G) {
-                const uint32_t ia = o + 4u * c2, ib = ia + 4u * hq2;
-                wa = row[(ia >> 5) << 6] >> (ia & 31u);
-                wb = row[(ib >> 5) << 6] >> (ib & 31u);
+                const uint32_t ia = 4u * c2, ib = ia + 4u * hq2;
+                wa = grp ? lw[0] >> gs : lb.at(ia);
+                wb = grp ? lw[1] >> gs : lb.at(ib);
             }
             // x[1] = alpha[s] chunk c2+hq pairs with x[0]; x[2], x[3] = chunks c2+hq2, c2+hq2+hq
             const float4 y0 = OPC == OP_F ? f4_f(x[0], x[1]) : f4_g(x[0], x[1], wa);
@@ -608,24 +769,26 @@ PCG_DEV void ls_fgf_op(Ls<LP>& c, uint32_t s, uint32_t o, uint32_t P)
 {
     const uint32_t d = s - 1, e = s - 2;
     const Share w = ls_share(c, P, s, 1u << (s - 4));
-    const uint32_t* row = c.row_of(w.dl);
+    const DBits lb = gbits(c, s, o, w.dl, w.bl);
     const uint32_t rm = ls_root_round(c, s, w.h);
+    const bool rootc = s >= c.mt && s != c.top, left = o < (c.N >> 1);
+    const DBits rb = rootc && !left ? root_bits(c, w) : DBits{};
     auto run = [&](auto dst2) {
         GlSt d1 = gl_st(c, d);
         d1.lane = w.dl;
         dst2.lane = w.dl;
         if (s == c.top)
-            ls_fgf<OPC, LP>(ChSt{ c.y }, d1, dst2, row, s, o, w);
-        else if (rm && o < (c.N >> 1))
-            ls_fgf_root<OPC, true, LP>(c, d1, dst2, row, s, o, w, rm);
+            ls_fgf<OPC, LP>(ChSt{ c.y }, d1, dst2, lb, s, w);
+        else if (rm && left)
+            ls_fgf_root<OPC, true, LP>(c, d1, dst2, lb, rb, s, w, rm);
         else if (rm)
-            ls_fgf_root<OPC, false, LP>(c, d1, dst2, row, s, o, w, rm);
-        else if (s >= c.mt && o < (c.N >> 1))
-            ls_fgf<OPC, LP>(RootSt<true>{ c.y, row, c.N >> 3 }, d1, dst2, row, s, o, w);
-        else if (s >= c.mt)
-            ls_fgf<OPC, LP>(RootSt<false>{ c.y, row, c.N >> 3 }, d1, dst2, row, s, o, w);
+            ls_fgf_root<OPC, false, LP>(c, d1, dst2, lb, rb, s, w, rm);
+        else if (rootc && left)
+            ls_fgf<OPC, LP>(RootSt<true>{ c.y, rb, c.N >> 3 }, d1, dst2, lb, s, w);
+        else if (rootc)
+            ls_fgf<OPC, LP>(RootSt<false>{ c.y, rb, c.N >> 3 }, d1, dst2, lb, s, w);
         else
-            ls_fgf<OPC, LP>(gl_st(c, s), d1, dst2, row, s, o, w);
+            ls_fgf<OPC, LP>(gl_st(c, s), d1, dst2, lb, s, w);
     };
     if (e >= c.Sl)
         run(gl_st(c, e));
@@ -635,36 +798,161 @@ PCG_DEV void ls_fgf_op(Ls<LP>& c, uint32_t s, uint32_t o, uint32_t P)
     c.own(e);
 }
 
-// Combine (avx_float.h:188-197 on packed bits): bit[o+i] ^= bit[o+h+i], i < h.
+// ---- node results into the D buffers ----------------------------------------------------
+// The 2^t result bits of the stage-t node at o go to the path's own lane: as its half of
+// D[t+1] (the parent's children), or as D[top] for the root.  d_word(w, v) stores result
+// word w (n = 2^t < 32: one call with the n bits, merged with the left half read from the
+// slot for a right child); d_end copies the left half of a multi-word right child over
+// from the slot, after every read of the op (the slot may be a lane that moves its own
+// left half here) and sets the table.  Every store follows the wave-wide read of the same
+// word, so lanes reading a column see it before its owner rewrites it.
 template <int LP>
-PCG_DEV void ls_comb(const Ls<LP>& c, uint32_t s, uint32_t o, bool act)
+PCG_DEV uint32_t d_target(const Ls<LP>& c, uint32_t t) { return t == c.top ? t : t + 1u; }
+
+// The word columns of one D stage (or of the LDS codeword region), LDS or global: distinct
+// types so that each copy loop is compiled for its own address space.
+struct DColL {
+    lds_u32* b;
+    PCG_DEV uint32_t ld(uint32_t w, uint32_t l) const { return b[(w << 6) + l]; }
+    PCG_DEV void st(uint32_t w, uint32_t l, uint32_t v) const { b[(w << 6) + l] = v; }
+};
+struct DColG {
+    gl_u32* b;
+    PCG_DEV uint32_t ld(uint32_t w, uint32_t l) const { return b[((uint64_t)w << 6) + l]; }
+    PCG_DEV void st(uint32_t w, uint32_t l, uint32_t v) const { b[((uint64_t)w << 6) + l] = v; }
+};
+template <int LP, typename Fn>
+PCG_DEV void with_d(const Ls<LP>& c, uint32_t s, Fn&& fn)
 {
-    const uint32_t h = 1u << (s - 1);
-    uint32_t* row = c.row();
-    if (!act)
-        return;
-    if (h >= 32) {
-        const uint32_t wl = o >> 5, wr = (o + h) >> 5, nw = h >> 5;
-        for (uint32_t w = 0; w < nw; ++w)
-            row[(wl + w) << 6] ^= row[(wr + w) << 6];
-    } else {
-        const uint32_t sh = o & 31u, msk = ((1u << h) - 1u) << sh;
-        uint32_t* w = row + ((o >> 5) << 6);
-        *w ^= (*w >> h) & msk;
+    const uint32_t o = ls_doff(s);
+    if (s < c.Sb)
+        fn(DColL{ c.dl + (o << 6) });
+    else
+        fn(DColG{ c.dg + ((uint64_t)(o - (1u << (c.Sb - 5u))) << 6) });
+}
+// words [0, nw) of lane sl's column -> this lane's column, 8 loads before their stores
+template <typename Col>
+PCG_DEV void d_copy(const Col& col, uint32_t nw, uint32_t sl, uint32_t lane)
+{
+    for (uint32_t w = 0; w < nw; w += 8) {
+        uint32_t x[8];
+#pragma unroll
+        for (uint32_t u = 0; u < 8; ++u)
+            if (w + u < nw)
+                x[u] = col.ld(w + u, sl);
+#pragma unroll
+        for (uint32_t u = 0; u < 8; ++u)
+            if (w + u < nw)
+                col.st(w + u, lane, x[u]);
     }
 }
 
-// Clear bits [o, o+n) of the lane's row (Rate-0: all-zero estimate).
 template <int LP>
-PCG_DEV void ls_clear(const Ls<LP>& c, uint32_t n, uint32_t o)
+PCG_DEV void d_word(const Ls<LP>& c, uint32_t t, uint32_t o, uint32_t w, uint32_t v)
 {
-    uint32_t* row = c.row();
-    if (n >= 32) {
-        for (uint32_t w = o >> 5; w < (o + n) >> 5; ++w)
-            row[w << 6] = 0u;
+    const uint32_t n = 1u << t, d = d_target(c, t);
+    if (d == t || ((o >> t) & 1u) == 0u) { // the root, or a left child
+        c.dst(d, w, v);
+    } else if (n < 32u) {
+        c.dst(d, 0, (c.dld(d, 0, c.dlane(d)) & ((1u << n) - 1u)) | (v << n));
     } else {
-        row[(o >> 5) << 6] &= ~(((1u << n) - 1u) << (o & 31u));
+        c.dst(d, (n >> 5) + w, v);
     }
+}
+template <int LP>
+PCG_DEV void d_end(Ls<LP>& c, uint32_t t, uint32_t o)
+{
+    const uint32_t n = 1u << t, d = d_target(c, t);
+    if (d != t && ((o >> t) & 1u) && n >= 32u) {
+        const uint32_t sl = c.dlane(d);
+        with_d(c, d, [&](const auto& col) { d_copy(col, n >> 5, sl, c.lane); });
+    }
+    c.down(d);
+}
+
+// Combine (avx_float.h:188-197 on packed bits) of the stage-s node at o: its children
+// D[s] = (l, r) give (l ^ r, r).  The root's codeword goes to the (now dead) LLR stage
+// region of LDS when it fits there (fin): the output stage reads it word by word.
+template <typename Src, typename Dst>
+PCG_DEV void comb_words(const Src& S, uint32_t sl, const Dst& T, uint32_t ob, uint32_t nw, uint32_t lane)
+{
+    for (uint32_t w = 0; w < nw; w += 8) {
+        uint32_t l[8], r[8];
+#pragma unroll
+        for (uint32_t u = 0; u < 8; ++u)
+            if (w + u < nw) {
+                l[u] = S.ld(w + u, sl);
+                r[u] = S.ld(nw + w + u, sl);
+            }
+#pragma unroll
+        for (uint32_t u = 0; u < 8; ++u)
+            if (w + u < nw) {
+                T.st(ob + w + u, lane, l[u] ^ r[u]);
+                T.st(ob + nw + w + u, lane, r[u]);
+            }
+    }
+}
+template <int LP>
+PCG_DEV void ls_comb(Ls<LP>& c, uint32_t s, uint32_t o, bool act)
+{
+    if constexpr (!Ls<LP>::DB) { // in the row: bit[o+i] ^= bit[o+h+i], i < h
+        const uint32_t h = 1u << (s - 1);
+        lds_u32* row = c.row();
+        if (!act)
+            return;
+        if (h >= 32) {
+            const uint32_t wl = o >> 5, wr = (o + h) >> 5, nw = h >> 5;
+            for (uint32_t w = 0; w < nw; ++w)
+                row[(wl + w) << 6] ^= row[(wr + w) << 6];
+        } else {
+            const uint32_t sh = o & 31u, msk = ((1u << h) - 1u) << sh;
+            lds_u32* w = row + ((o >> 5) << 6);
+            *w ^= (*w >> h) & msk;
+        }
+        return;
+    }
+    const uint32_t h = 1u << (s - 1), sl = c.dlane(s);
+    const bool root = s == c.top;
+    if (root && h >= 32u && c.Sl > 3u + c.vlow && (h >> 4) <= (1u << c.Sl) - c.ab) {
+        c.fin = true;
+        if (act)
+            with_d(c, s, [&](const auto& S) {
+                comb_words(S, sl, DColL{ (lds_u32*)(c.lds + c.ly.alpha) }, 0u, h >> 5, c.lane);
+            });
+        return;
+    }
+    if (!act)
+        return;
+    if (h < 32u) { // s = 4, 5: one word
+        const uint32_t x = c.dld(s, 0, sl), m = (1u << h) - 1u;
+        d_word(c, s, o, 0, ((x ^ (x >> h)) & m) | (x & (m << h)));
+    } else {
+        const uint32_t d = d_target(c, s), ob = !root && ((o >> s) & 1u) ? h >> 4 : 0u;
+        with_d(c, s, [&](const auto& S) {
+            with_d(c, d, [&](const auto& T) { comb_words(S, sl, T, ob, h >> 5, c.lane); });
+        });
+    }
+    d_end(c, s, o);
+}
+
+// Rate-0: the all-zero estimate.
+template <int LP>
+PCG_DEV void ls_clear(Ls<LP>& c, uint32_t t, uint32_t o)
+{
+    const uint32_t n = 1u << t;
+    if constexpr (!Ls<LP>::DB) { // bits [o, o+n) of the row
+        lds_u32* row = c.row();
+        if (n >= 32) {
+            for (uint32_t w = o >> 5; w < (o + n) >> 5; ++w)
+                row[w << 6] = 0u;
+        } else {
+            row[(o >> 5) << 6] &= ~(((1u << n) - 1u) << (o & 31u));
+        }
+        return;
+    }
+    for (uint32_t w = 0; w < (n >= 32u ? n >> 5 : 1u); ++w)
+        d_word(c, t, o, w, 0u);
+    d_end(c, t, o);
 }
 
 // ---- Rate-0 leaf, n >= 8 (scl_avx_float.cpp:316-337) ----------------------------------
@@ -700,7 +988,7 @@ PCG_DEV void ls_r0(Ls<LP>& c, Src src, uint32_t s, uint32_t o, bool act)
     for (int j = 1; j < 8; ++j)
         r = r + acc[j];
     c.m = c.m + r;
-    ls_clear(c, 1u << s, o);
+    ls_clear(c, s, o);
 }
 
 // ---- weak positions: findWeakLlrs(idx, |llr|, n, kk) (arrayfuncs.h:209-231) ------------
@@ -1216,8 +1504,9 @@ PCG_DEV void ls_select(const Ls<LP>& c, const float (&cv)[8], uint32_t P, uint32
     wsync();
 }
 
-// Duplicate the LDS path state of path `srcp` into this lane: slot table row and
-// codeword words [0, nw).  Converged code (bpermute); act = this lane survives.
+// This lane takes the state of path `srcp`: its slot tables -- the LLR stages (and D
+// bits) live on where they are (DataPool's lazy copy) -- and, with codeword rows, the row
+// words [0, nw) decoded so far.  Converged code (bpermute); act = this lane survives.
 template <int LP>
 PCG_DEV void ls_dup(Ls<LP>& c, uint32_t srcp, uint32_t nw, bool act)
 {
@@ -1225,26 +1514,31 @@ PCG_DEV void ls_dup(Ls<LP>& c, uint32_t srcp, uint32_t nw, bool act)
     const int sl = (int)(c.gb | srcp);
     const uint32_t lo = shfl((uint32_t)c.ptr, sl), hi = shfl((uint32_t)(c.ptr >> 32), sl);
     c.ptr = ((uint64_t)hi << 32) | lo;
-    const uint32_t* srow = c.row_of((uint32_t)sl);
-    uint32_t* row = c.row();
-    // one wave's LDS instructions execute in order: every lane's read of a word
-    // completes before any lane's write of it; 8 reads are issued before their writes
-    uint32_t w = 0;
-    for (; w + 8 <= nw; w += 8) {
-        uint32_t x[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            x[u] = srow[(w + u) << 6];
-        if (act) {
+    if constexpr (Ls<LP>::DB) {
+        const uint32_t blo = shfl((uint32_t)c.bptr, sl), bhi = shfl((uint32_t)(c.bptr >> 32), sl);
+        c.bptr = ((uint64_t)bhi << 32) | blo;
+    } else {
+        const lds_u32* srow = c.row_of((uint32_t)sl);
+        lds_u32* row = c.row();
+        // one wave's LDS instructions execute in order: every lane's read of a word
+        // completes before any lane's write of it; 8 reads are issued before their writes
+        uint32_t w = 0;
+        for (; w + 8 <= nw; w += 8) {
+            uint32_t x[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u)
-                row[(w + u) << 6] = x[u];
+                x[u] = srow[(w + u) << 6];
+            if (act) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    row[(w + u) << 6] = x[u];
+            }
         }
-    }
-    for (; w < nw; ++w) {
-        const uint32_t x = srow[w << 6];
-        if (act)
-            row[w << 6] = x;
+        for (; w < nw; ++w) {
+            const uint32_t x = srow[w << 6];
+            if (act)
+                row[w << 6] = x;
+        }
     }
     LS_STAMP(c, 51);
 }
@@ -1298,9 +1592,8 @@ PCG_DEV void ls_branch_leaf(Ls<LP>& c, Src src, uint32_t code, uint32_t s, uint3
         return;
     c.m = val;
     const uint32_t fm = ls_flip_sel(code, j, pars & 0x80000000u ? 1u : 0u);
-    // hard decisions of the source path's leaf LLRs (its slot via the copied row)
+    // hard decisions of the source path's leaf LLRs (its slot via the copied table)
     const uint32_t sl2 = s == c.top ? 0u : c.src_lane(s);
-    uint32_t* row = c.row();
     for (uint32_t w0 = 0; w0 < n; w0 += 32) {
         const uint32_t nb = n < 32 ? n : 32u;
         uint32_t word = 0;
@@ -1321,15 +1614,22 @@ PCG_DEV void ls_branch_leaf(Ls<LP>& c, Src src, uint32_t code, uint32_t s, uint3
         for (int t = 0; t < 4; ++t)
             if (((fm >> t) & 1u) && Is[t] >= w0 && Is[t] < w0 + nb)
                 word ^= 1u << (Is[t] - w0);
-        const uint32_t pos = o + w0;
-        if (nb == 32) {
-            row[(pos >> 5) << 6] = word;
+        if constexpr (Ls<LP>::DB) {
+            d_word(c, s, o, w0 >> 5, word);
         } else {
-            const uint32_t sh = pos & 31u, msk = ((1u << nb) - 1u) << sh;
-            uint32_t* wp = row + ((pos >> 5) << 6);
-            *wp = (*wp & ~msk) | (word << sh);
+            lds_u32* row = c.row();
+            const uint32_t pos = o + w0;
+            if (nb == 32) {
+                row[(pos >> 5) << 6] = word;
+            } else {
+                const uint32_t sh = pos & 31u, msk = ((1u << nb) - 1u) << sh;
+                lds_u32* wp = row + ((pos >> 5) << 6);
+                *wp = (*wp & ~msk) | (word << sh);
+            }
         }
     }
+    if constexpr (Ls<LP>::DB)
+        d_end(c, s, o);
 }
 
 // ---- size-8 subtrees in registers (ShortRateRNode(8), scl_avx_float.cpp:273-307) -----
@@ -1540,15 +1840,20 @@ PCG_DEV void ls_st8(Ls<LP>& c, Src src, uint32_t desc, uint32_t o, uint32_t& P)
         st.a4[i] = polar_g(st.x8[i], st.x8[i + 4], ((st.bits >> i) & 1u) << 31);
     st8_child4(c, st, (desc >> 8) & 0xffu, 4);
     st.bits ^= (st.bits >> 4) & 0xFu; // CombineBitsShort(4)
-    // write back the 8 bits at [o, o+8); after branching, first take the LDS path
-    // state (slot table, codeword prefix) of the path each survivor descends from
+    // the 8 bits into D[4] or the row; after branching, first take the state (slot tables,
+    // row prefix) of the path each survivor descends from
     const uint32_t sh = o & 31u, wo = o >> 5, msk = 0xFFu << sh;
     if (st.branched)
         ls_dup(c, st.root, wo + 1, c.p < st.P);
     P = st.P;
     if (c.p < P) {
-        uint32_t* w = c.row() + (wo << 6);
-        *w = (*w & ~msk) | (st.bits << sh);
+        if constexpr (Ls<LP>::DB) {
+            d_word(c, 3, o, 0, st.bits);
+            d_end(c, 3, o);
+        } else {
+            lds_u32* w = c.row() + (wo << 6);
+            *w = (*w & ~msk) | (st.bits << sh);
+        }
     }
 }
 
@@ -1557,14 +1862,15 @@ PCG_DEV void ls_st8(Ls<LP>& c, Src src, uint32_t desc, uint32_t o, uint32_t& P)
 // bit r of it is c0_r ^ parity(sum_w popcount(word_w & rows[r][w])): W * CB and +
 // popcount pairs per lane, the masks wave-uniform scalar loads.
 template <int CB>
-PCG_DEV uint32_t crc_syn(const uint32_t* row, const uint32_t* rows, uint32_t W, uint32_t c0)
+PCG_DEV uint32_t crc_syn(const DBits& cw, const uint32_t* rows, uint32_t W, uint32_t c0)
 {
     uint32_t acc[CB];
 #pragma unroll
     for (int r = 0; r < CB; ++r)
         acc[r] = 0;
+#pragma unroll 4
     for (uint32_t w = 0; w < W; ++w) {
-        const uint32_t word = row[w << 6];
+        const uint32_t word = cw.word(w);
 #pragma unroll
         for (int r = 0; r < CB; ++r)
             acc[r] += (uint32_t)__builtin_popcount(word & ld_const(rows, r * W + w));
@@ -1602,13 +1908,16 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
     c.mt = ls_mtop(c.top, a.scl_virt);
     c.vlow = a.scl_v3;
     c.ab = ls_abase(c.vlow);
-    c.ly = ls_layout(a.N, a.lds_stage_limit, c.vlow);
+    c.Sb = a.scl_sb;
+    c.ly = ls_layout(c.top, a.lds_stage_limit, c.vlow, c.Sb);
     c.lane = threadIdx.x;
     c.share = (a.scl_fuse >> 1) & 1u;
     c.stage_root = (a.scl_fuse >> 2) & 1u;
     c.p = c.lane & (LP - 1);
     c.gb = c.lane & ~(uint32_t)(LP - 1);
     c.gs = a.scratch + (uint64_t)blockIdx.x * a.scratch_floats;
+    c.dl = (lds_u32*)(smem + c.ly.d);
+    c.dg = (gl_u32*)(c.gs + ls_gl_alpha_floats(c.mt, c.Sl) + 1024u); // after the tie region
     const uint32_t W = a.N >= 32 ? a.N / 32 : 1u;
 
     const uint64_t Fn = a.fcount ? (uint64_t)*a.fcount : a.F;
@@ -1626,6 +1935,8 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
         // instance, at the previous frame's final path-0 metric
         c.m = a.metric0;
         c.ptr = 0;
+        c.bptr = 0;
+        c.fin = false;
         uint32_t P = 1;
 #ifdef PCG_LS_PROF
         const uint64_t tf0 = __builtin_amdgcn_s_memtime();
@@ -1692,29 +2003,48 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
 #endif
         // extractBestPath (scl_avx_float.cpp:711-750): first path in list order whose
         // detector check passes, else path 0.
+        // (every active path's codeword is in its own lane: the root's op wrote it, to D[top]
+        // or, fin, to the LDS stage region)
         const bool act = c.p < P;
-        uint32_t* row = c.row();
+        const uint32_t top = c.top;
+        const lds_u32* fr = (const lds_u32*)(c.lds + c.ly.alpha);
+        auto cw_of = [&](uint32_t l) {
+            if constexpr (!Ls<LP>::DB)
+                return rowbits(c, l, 0u);
+            return c.fin ? DBits{ fr, nullptr, l, false, 0u } : dbits(c, top, l);
+        };
         if (!a.systematic && act) {
+            lds_u32* f = Ls<LP>::DB ? (lds_u32*)(c.lds + c.ly.alpha) + c.lane : c.row();
+            const bool lf = !Ls<LP>::DB || c.fin;
+            auto ld = [&](uint32_t wi) { return lf ? f[wi << 6] : c.dld(top, wi, c.lane); };
+            auto st = [&](uint32_t wi, uint32_t v) {
+                if (lf)
+                    f[wi << 6] = v;
+                else
+                    c.dst(top, wi, v);
+            };
             for (uint32_t wi = 0; wi < W; ++wi)
-                row[wi << 6] = transform_word(row[wi << 6], a.N);
+                st(wi, transform_word(ld(wi), a.N));
             for (uint32_t d = 1; d < W; d <<= 1)
                 for (uint32_t wi = 0; wi < W; ++wi)
                     if (!(wi & d))
-                        row[wi << 6] ^= row[(wi + d) << 6];
+                        st(wi, ld(wi) ^ ld(wi + d));
         }
+        wsync();
         // detector syndrome: bit r = c0_r ^ parity(codeword & row mask r)
+        const DBits cw = cw_of(c.lane);
         uint32_t syn;
         switch (a.crc_bits) {
-        case 8: syn = crc_syn<8>(row, a.crc_rows, W, a.crc_c0); break;
-        case 11: syn = crc_syn<11>(row, a.crc_rows, W, a.crc_c0); break;
-        case 16: syn = crc_syn<16>(row, a.crc_rows, W, a.crc_c0); break;
-        case 32: syn = crc_syn<32>(row, a.crc_rows, W, a.crc_c0); break;
+        case 8: syn = crc_syn<8>(cw, a.crc_rows, W, a.crc_c0); break;
+        case 11: syn = crc_syn<11>(cw, a.crc_rows, W, a.crc_c0); break;
+        case 16: syn = crc_syn<16>(cw, a.crc_rows, W, a.crc_c0); break;
+        case 32: syn = crc_syn<32>(cw, a.crc_rows, W, a.crc_c0); break;
         default: syn = a.crc_c0; break;
         }
         const uint64_t okm = ballot(act && syn == 0u);
         const uint32_t gm = (uint32_t)((okm >> c.gb) & (LP == 64 ? ~0ull : ((1ull << LP) - 1ull)));
         const uint32_t chosen = gm ? (uint32_t)__builtin_ctz(gm) : 0u;
-        const uint32_t* crow = c.row_of(c.gb | chosen);
+        const DBits crow = cw_of(c.gb | chosen);
         if (fvalid) {
             for (uint32_t b = c.p; b < a.kb; b += LP) {
                 uint32_t byte = 0;
@@ -1722,7 +2052,7 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
                     const uint32_t idx = 8 * b + j;
                     if (idx < a.K) {
                         const uint32_t ps = a.info_pos[idx];
-                        byte |= ((crow[(ps >> 5) << 6] >> (ps & 31u)) & 1u) << (7 - j);
+                        byte |= (crow.at(ps) & 1u) << (7 - j);
                     }
                 }
                 a.info[frame * a.kb + b] = (uint8_t)byte;
@@ -1753,9 +2083,10 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
 
 } // namespace
 
-int sclls_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* lds_stage_limit,
-                 uint64_t* scratch_floats, uint32_t* virt, uint32_t* v3)
+int sclls_layout(uint32_t N, uint32_t L, uint32_t lp, uint32_t* wave_lds_floats, uint32_t* lds_stage_limit,
+                 uint64_t* scratch_floats, uint32_t* virt, uint32_t* v3, uint32_t* sb)
 {
+    const bool db = lp >= PCG_LS_DBITS_LP;
     if (L < 2 || L > 32 || N < 8)
         return -4;
     const uint32_t top = (uint32_t)__builtin_ctz(N);
@@ -1768,10 +2099,13 @@ int sclls_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* ld
         const uint32_t v = (uint32_t)atoi(e);
         w3 = v == 0 ? 0u : (v >= 2 && top >= 7 ? 2u : w3);
     }
-    uint32_t budget = 24 * 1024 / 4; // floats per wave (N = 1024, L = 8: S_l = 6, stages 4-5 in LDS: 20 KB, 8 waves/CU)
+    // floats per wave.  Rows: 24 KB (N = 1024, L = 8: S_l = 6, stages 4-5 and the rows in
+    // LDS: 20 KB, 8 waves/CU); D buffers: 20 KB = 8 waves/CU, the VGPR limit too (N = 4096:
+    // LLR stages 4-5 and D stages 4-9)
+    uint32_t budget = (db ? 20 : 24) * 1024 / 4;
     const uint32_t bitsf = 64u * (N >= 32 ? N / 32 : 1u);
-    if (bitsf + 2048u > budget) // large N: the bit rows alone fill 24 KB; keep stages 3-4 on chip
-        budget = bitsf + 2048u;  // (N = 4096: 40 KB, 4 waves/CU: +3 % over 24 KB, r02y sweep)
+    if (!db && bitsf + 2048u > budget) // large N: the rows alone fill 24 KB; keep stages 3-4 on chip
+        budget = bitsf + 2048u;
     if (const char* e = getenv("PCG_SCL_LDS_KB"))
         budget = (uint32_t)atoi(e) * 1024 / 4;
     uint32_t vt = ls_max_virt(top);
@@ -1780,22 +2114,34 @@ int sclls_layout(uint32_t N, uint32_t L, uint32_t* wave_lds_floats, uint32_t* ld
         vt = v < vt ? v : vt;
     }
     const uint32_t mt = ls_mtop(top, vt);
+    // LDS: the small D stages (4-7: every leaf and Combine writes one), then LLR stages up
+    // from 3+v3, then the larger D stages while they fit
+    uint32_t Sb = top + 1 < 8u ? top + 1 : 8u;
+    Sb = !db ? 0u : (Sb < 5u ? 5u : Sb);
     uint32_t Sl = mt;
-    while (Sl > LS_MINS && ls_layout(N, Sl, w3).total > budget)
+    while (Sl > LS_MINS && ls_layout(top, Sl, w3, Sb).total > budget)
         --Sl;
     if (const char* e = getenv("PCG_SCL_STAGE_LIMIT")) {
         const uint32_t v = (uint32_t)atoi(e);
         if (v >= LS_MINS && v <= mt)
             Sl = v;
     }
-    const LsLayout ly = ls_layout(N, Sl, w3);
+    while (db && Sb <= top && ls_layout(top, Sl, w3, Sb + 1).total <= budget)
+        ++Sb;
+    if (const char* e = getenv("PCG_SCL_SB"); e && db) {
+        const uint32_t v = (uint32_t)atoi(e);
+        if (v >= 5 && v <= top + 1)
+            Sb = v;
+    }
+    const LsLayout ly = ls_layout(top, Sl, w3, Sb);
     if (ly.total * 4 > 160 * 1024)
         return -4;
     *wave_lds_floats = ly.total;
     *lds_stage_limit = Sl;
-    *scratch_floats = ls_gl_alpha_floats(mt, Sl) + 1024;
+    *scratch_floats = ls_gl_alpha_floats(mt, Sl) + 1024 + 64ull * ls_dgl_words(top, Sb);
     *virt = vt;
     *v3 = w3;
+    *sb = Sb;
     return 0;
 }
 
