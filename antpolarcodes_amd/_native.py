@@ -40,6 +40,7 @@ class PlanDesc(C.Structure):
         ("systematic", C.c_int32),
         ("lanes_per_codeword", C.c_uint32),
         ("dev_overrides", C.c_uint32),  # PCG_DEV_* bits: non-default kernel/layout from dev env switches
+        ("recomputed_stages", C.c_uint32),  # lane-serial SCL: top stages recomputed (1 or 2)
     ]
 
 

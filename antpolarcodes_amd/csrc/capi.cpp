@@ -82,6 +82,21 @@ int hip_fail(hipError_t e, const char* what)
     return fail(PCG_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// Every SCL node of stage >= top-2 internal (no leaf or size-8 subtree op there): the
+// condition for recomputing the quarters of the codeword inside their staged F/G ops
+// (sclls_layout, virt = 2).
+bool scl_top_nodes_internal(const std::vector<uint32_t>& ops, uint32_t top)
+{
+    for (size_t k = 0; k < ops.size(); ++k) {
+        const uint32_t c = pcg::op_code(ops[k]), s = pcg::op_stage(ops[k]);
+        if (c >= pcg::OP_S_R0 && c <= pcg::OP_S_ST8 && s + 2u >= top)
+            return false;
+        if (c == pcg::OP_S_ST8)
+            ++k; // its descriptor word
+    }
+    return true;
+}
+
 struct DeviceGuard {
     int prev = 0;
     bool ok = false;
@@ -324,12 +339,13 @@ static int plan_create_impl(pcg_plan** out,
         p->scl_lp = list_pow2(L);
         if (scl_lp > p->scl_lp && scl_lp <= 32 && (scl_lp & (scl_lp - 1)) == 0)
             p->scl_lp = scl_lp;
-        rc = pcg::sclls_layout(N, L, p->scl_lp, &p->wave_lds_floats, &p->lds_stage_limit, &p->scratch_floats,
-                               &p->scl_virt, &p->scl_v3, &p->scl_sb);
         if (const char* e = getenv("PCG_SCL_FUSE")) {
             p->scl_fuse = (uint32_t)atoi(e);
             p->dev_overrides |= PCG_DEV_SCL_FUSE;
         }
+        const bool quarters_ok = (p->scl_fuse & 5u) == 5u && scl_top_nodes_internal(p->host.ops, p->host.log2N);
+        rc = pcg::sclls_layout(N, L, p->scl_lp, quarters_ok, &p->wave_lds_floats, &p->lds_stage_limit,
+                               &p->scratch_floats, &p->scl_virt, &p->scl_v3, &p->scl_sb);
         if (rc != 0) {
             delete p;
             return fail(rc, "list decoding layout unsupported for this N/L");
@@ -542,6 +558,7 @@ int pcg_plan_describe(const pcg_plan* p, pcg_plan_desc* d)
     d->lanes_per_codeword = p->host.L > 1 && !p->host.fixed ? p->scl_lp
                           : (p->host.L == 1 && p->host.sc_kind == 2 ? p->host.scq_q : 0);
     d->dev_overrides = p->dev_overrides | (p->fast ? p->fast->dev_overrides : 0u);
+    d->recomputed_stages = p->host.L > 1 && !p->host.fixed ? p->scl_virt : 0u;
     return PCG_OK;
 }
 

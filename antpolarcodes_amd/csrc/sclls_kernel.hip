@@ -76,7 +76,7 @@ __host__ __device__ inline uint32_t ls_mtop(uint32_t top, uint32_t virt)
     const uint32_t m = top - virt;
     return m > 3u ? m : 3u;
 }
-__host__ __device__ inline uint32_t ls_max_virt(uint32_t top) { return top >= 4 ? 1u : 0u; }
+__host__ __device__ inline uint32_t ls_max_virt(uint32_t top) { return top >= 7 ? 2u : (top >= 4 ? 1u : 0u); }
 
 // Global scratch slab of one wave: alpha stages [Sl, mtop), then the tie-fallback
 // candidate list (64 * 8 values + 64 * 8 ids; rarely touched, so not worth LDS).
@@ -281,6 +281,8 @@ struct RootSt { // stage top-1, left or right child of the root
         return f4_g(a, b, lb.at(4u * c));
     }
 };
+// virt = 2: stage top-2 (the root's grandchildren, quarter q of the codeword) is recomputed
+// from four channel chunks, only inside the staged fused op (ls_fgf_root2).
 // Any recomputed stage behind one wave-uniform switch (leaves and size-8 subtrees at
 // stage top or top-1: rare, so one instantiation serves all of them).
 // (The left bits are read through the live context: a survivor's reload after ls_dup
@@ -289,7 +291,7 @@ template <int LP>
 struct VirtSt {
     const Ls<LP>* cp;
     uint32_t hq1;
-    bool root, left;
+    bool root, left; // root: a child of the root (else the channel); left: the left one
     PCG_DEV float4 ld(uint32_t c, uint32_t l) const
     {
         if (!root)
@@ -302,6 +304,7 @@ struct VirtSt {
             return RootSt<false>{ cp->y, rowbits(*cp, cp->lane, 0u), hq1 }.ld(c, l);
     }
 };
+// (virt = 2 is only planned when no leaf sits at stage top-2 or above: sclls_layout.)
 
 // prefetch depth (float4 chunks per batch) of the streaming loops for a storage
 template <typename S>
@@ -515,6 +518,15 @@ PCG_DEV DBits root_bits(const Ls<LP>& c, const Share& w)
     else
         return rowbits(c, w.dl, 0u);
 }
+// the bits of the left child of the top-1 node holding the quarter at o (virt = 2)
+template <int LP>
+PCG_DEV DBits mid_bits(const Ls<LP>& c, const Share& w, uint32_t o)
+{
+    if constexpr (Ls<LP>::DB)
+        return dbits(c, c.top - 1u, w.shr ? path_dlane(c, w.dl, c.top - 1u) : c.dlane(c.top - 1u));
+    else
+        return rowbits(c, w.dl, o & ~((c.N >> 1) - 1u));
+}
 template <typename S>
 struct Off { // chunks [b, ...) of a storage
     S s;
@@ -580,8 +592,25 @@ PCG_DEV void ls_fg_op(Ls<LP>& c, uint32_t s, uint32_t o, uint32_t P)
     const uint32_t d = s - 1;
     if (d >= c.mt || d < 3u + c.vlow) // recomputed where it is read
         return;
-    const Share w = ls_share(c, P, s, 1u << (s - 3));
+    const bool quarter = s >= c.mt && s + 2u == c.top;
+    const Share w = ls_share(c, P, s, quarter ? 0u : 1u << (s - 3)); // (quarters: one lane per path)
     const DBits lb = gbits(c, s, o, w.dl, w.bl);
+    if (quarter) { // a quarter whose child is a leaf: staged, unfused (alpha[s-1] is global)
+        const uint32_t rm = ls_root_round(c, s, w.h, false);
+        if (rm) { // (always: sclls_layout plans virt = 2 only when it stages)
+            const DBits qr = root_bits(c, w), qm = mid_bits(c, w, o);
+            GlSt d1 = gl_st(c, d);
+            d1.lane = w.dl;
+            switch (o / (c.N >> 2)) {
+            case 0: ls_fgf_root2<OPC, false, false, false, LP>(c, d1, d1, lb, qr, qm, s, w, rm); break;
+            case 1: ls_fgf_root2<OPC, false, true, false, LP>(c, d1, d1, lb, qr, qm, s, w, rm); break;
+            case 2: ls_fgf_root2<OPC, true, false, false, LP>(c, d1, d1, lb, qr, qm, s, w, rm); break;
+            default: ls_fgf_root2<OPC, true, true, false, LP>(c, d1, d1, lb, qr, qm, s, w, rm); break;
+            }
+        }
+        c.own(d);
+        return;
+    }
     auto run = [&](auto dst) {
         dst.lane = w.dl;
         if (s == c.top)
@@ -751,35 +780,128 @@ PCG_DEV void ls_fgf_root(const Ls<LP>& c, GlSt d1, Dst2 d2, const DBits& lb, con
 // Output chunks per staging round of ls_fgf_root, or 0 when it does not apply: the
 // LDS stages' region must hold a round, hold no output, and give every lane a chunk.
 template <int LP>
-PCG_DEV uint32_t ls_root_round(const Ls<LP>& c, uint32_t s, uint32_t h)
+PCG_DEV uint32_t ls_root_round(const Ls<LP>& c, uint32_t s, uint32_t h, bool fused = true)
 {
-    if (!c.stage_root || s != c.mt || s == c.top || s - 2 < c.Sl || (1u << c.Sl) <= c.ab)
+    // (unfused: only the quarters' X, whose output alpha[s-1] must not be in the region)
+    if (!c.stage_root || s != c.mt || s == c.top || s - (fused ? 2u : 1u) < c.Sl || (1u << c.Sl) <= c.ab)
         return 0;
-    const uint32_t hq2 = 1u << (s - 4);
     const uint32_t region = 4u * 64u * ((1u << c.Sl) - c.ab); // bytes
-    uint32_t m = hq2;
-    while (m > 1 && (64u / LP) * 8u * m * 16u > region)
+    const uint32_t k = s + 2u == c.top ? (fused ? 16u : 8u) : 8u; // channel chunks per output chunk
+    uint32_t m = fused ? 1u << (s - 4) : 1u << (s - 3);          // output chunks of the op
+    while (m > 1 && (64u / LP) * k * m * 16u > region)
         m >>= 1;
-    const uint32_t need = h > LP / 8u ? h : LP / 8u;
-    return (64u / LP) * 8u * m * 16u <= region && m >= need && m >= 1 ? m : 0u;
+    const uint32_t need = h > LP / k ? h : LP / k;
+    return (64u / LP) * k * m * 16u <= region && m >= need && m >= 1 ? m : 0u;
+}
+
+// virt = 2: the fused op on a quarter (s = top-2), staged like ls_fgf_root with 16 channel
+// chunks per output chunk -- alpha[s] chunk a_k (k < 4: c2, c2+hq, c2+hq2, c2+hq2+hq) from
+// the channel chunks a_k + {0, N/8, N/16, N/16+N/8} at staged index 16u + 4k + j.  Bits: the
+// root's left half (R1), the top-1 node's left child (R2), the op's own G bits.
+// FU = false: the X alone (its child is a leaf): output chunk c2 < hq of alpha[s-1] from
+// alpha[s] chunks c2, c2+hq (8 staged chunks each, 4k + j, k < 2).
+template <int OPC, bool R1, bool R2, bool FU, int LP, typename Dst2>
+PCG_DEV void ls_fgf_root2(const Ls<LP>& c, GlSt d1, Dst2 d2, const DBits& lb, const DBits& rb, const DBits& mb,
+                          uint32_t s, const Share& w, uint32_t m)
+{
+    constexpr uint32_t KS = FU ? 4u : 2u; // alpha[s] chunks per output chunk
+    const uint32_t hq = 1u << (s - 3), hq2 = hq >> 1, h8 = c.N >> 3, h16 = c.N >> 4;
+    const uint32_t nout = FU ? hq2 : hq;  // output chunks of the op
+    float* stg = c.lds + c.ly.alpha;
+    const uint32_t per = 4u * KS * m;              // chunks per codeword per round
+    const uint32_t ninst = (64u / LP) * per / 64u; // DMA instructions per round
+    const uint32_t n = m / w.h;                    // output chunks per lane per round
+    const uint64_t yp = (uint64_t)(uintptr_t)c.y;
+    const float4* mine = reinterpret_cast<const float4*>(stg) + (c.lane / LP) * per;
+    // bit words of 8 aligned output chunks (s >= 7, N >= 128: every offset a multiple of 8)
+    uint32_t rw[4][2] = { { 0, 0 }, { 0, 0 }, { 0, 0 }, { 0, 0 } }, mw[4] = { 0, 0, 0, 0 }, lw[2] = { 0, 0 };
+    auto words = [&](uint32_t cg) {
+#pragma unroll
+        for (uint32_t k = 0; k < KS; ++k) {
+            const uint32_t a = cg + ((k & 1) ? hq : 0u) + ((k & 2) ? hq2 : 0u);
+            if (R1) {
+                rw[k][0] = rb.wat(4u * a);
+                rw[k][1] = rb.wat(4u * (a + h16));
+            }
+            if (R2)
+                mw[k] = mb.wat(4u * a);
+        }
+        if (OPC == OP_G) {
+            lw[0] = lb.wat(4u * cg);
+            if (FU)
+                lw[1] = lb.wat(4u * (cg + hq2));
+        }
+    };
+    for (uint32_t r = 0; r < nout; r += m) {
+        __builtin_amdgcn_s_waitcnt(0); // the previous round's LDS reads have completed
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t t = 0; t < ninst; ++t) {
+            const uint32_t f = t * 64u + c.lane;
+            const uint32_t g = f / per, rem = f % per, u = rem / (4u * KS), k = (rem >> 2) % KS, j = rem & 3u;
+            uint32_t a = r + u + ((k & 1u) ? hq : 0u) + ((k & 2u) ? hq2 : 0u);
+            a += ((j & 1u) ? h8 : 0u) + ((j & 2u) ? h16 : 0u);
+            const uint32_t lo = shfl((uint32_t)yp, (int)(g * LP)), hi = shfl((uint32_t)(yp >> 32), (int)(g * LP));
+            const float* src = reinterpret_cast<const float*>((uintptr_t)(((uint64_t)hi << 32) | lo)) + 4u * a;
+            __builtin_amdgcn_global_load_lds(src, stg + t * 256u, 16, 0, 0);
+        }
+        if (w.act)
+            words(r + w.i * n);
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_wave_barrier();
+        if (!w.act)
+            continue;
+        for (uint32_t uu = 0; uu < n; ++uu) {
+            const uint32_t u = w.i * n + uu, c2 = r + u;
+            if (uu > 0 && (uu & 7u) == 0)
+                words(c2);
+            const uint32_t gs = 4u * (c2 & 7u);
+            float4 x[KS];
+#pragma unroll
+            for (uint32_t k = 0; k < KS; ++k) {
+                const uint32_t b = u * 4u * KS + 4u * k;
+                const float4 y0 = mine[b], y1 = mine[b + 1u], y2 = mine[b + 2u], y3 = mine[b + 3u];
+                const float4 b0 = R1 ? f4_g(y0, y1, rw[k][0] >> gs) : f4_f(y0, y1);
+                const float4 b1 = R1 ? f4_g(y2, y3, rw[k][1] >> gs) : f4_f(y2, y3);
+                x[k] = R2 ? f4_g(b0, b1, mw[k] >> gs) : f4_f(b0, b1);
+            }
+            const float4 y0 = OPC == OP_F ? f4_f(x[0], x[1]) : f4_g(x[0], x[1], lw[0] >> gs);
+            d1.st(c2, y0);
+            if constexpr (FU) {
+                const float4 y1 = OPC == OP_F ? f4_f(x[2], x[3]) : f4_g(x[2], x[3], lw[1] >> gs);
+                d1.st(c2 + hq2, y1);
+                d2.st(c2, f4_f(y0, y1));
+            }
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0);
 }
 
 template <int OPC, int LP>
 PCG_DEV void ls_fgf_op(Ls<LP>& c, uint32_t s, uint32_t o, uint32_t P)
 {
     const uint32_t d = s - 1, e = s - 2;
-    const Share w = ls_share(c, P, s, 1u << (s - 4));
+    const bool rootc = s >= c.mt && s != c.top, left = o < (c.N >> 1), quarter = rootc && s + 2u == c.top;
+    const Share w = ls_share(c, P, s, quarter ? 0u : 1u << (s - 4)); // (quarters: one lane per path)
     const DBits lb = gbits(c, s, o, w.dl, w.bl);
     const uint32_t rm = ls_root_round(c, s, w.h);
-    const bool rootc = s >= c.mt && s != c.top, left = o < (c.N >> 1);
-    const DBits rb = rootc && !left ? root_bits(c, w) : DBits{};
+    const DBits rb = rootc && !left && !quarter ? root_bits(c, w) : DBits{};
     auto run = [&](auto dst2) {
         GlSt d1 = gl_st(c, d);
         d1.lane = w.dl;
         dst2.lane = w.dl;
-        if (s == c.top)
+        if (s == c.top) {
             ls_fgf<OPC, LP>(ChSt{ c.y }, d1, dst2, lb, s, w);
-        else if (rm && left)
+        } else if (quarter && rm) {
+            const DBits qr = root_bits(c, w), qm = mid_bits(c, w, o);
+            switch (o / (c.N >> 2)) {
+            case 0: ls_fgf_root2<OPC, false, false, true, LP>(c, d1, dst2, lb, qr, qm, s, w, rm); break;
+            case 1: ls_fgf_root2<OPC, false, true, true, LP>(c, d1, dst2, lb, qr, qm, s, w, rm); break;
+            case 2: ls_fgf_root2<OPC, true, false, true, LP>(c, d1, dst2, lb, qr, qm, s, w, rm); break;
+            default: ls_fgf_root2<OPC, true, true, true, LP>(c, d1, dst2, lb, qr, qm, s, w, rm); break;
+            }
+        } else if (quarter) {
+            return; // (unreachable: sclls_layout plans virt = 2 only when this op stages)
+        } else if (rm && left)
             ls_fgf_root<OPC, true, LP>(c, d1, dst2, lb, rb, s, w, rm);
         else if (rm)
             ls_fgf_root<OPC, false, LP>(c, d1, dst2, lb, rb, s, w, rm);
@@ -790,6 +912,7 @@ PCG_DEV void ls_fgf_op(Ls<LP>& c, uint32_t s, uint32_t o, uint32_t P)
         else
             ls_fgf<OPC, LP>(gl_st(c, s), d1, dst2, lb, s, w);
     };
+    (void)quarter;
     if (e >= c.Sl)
         run(gl_st(c, e));
     else
@@ -2083,8 +2206,11 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
 
 } // namespace
 
-int sclls_layout(uint32_t N, uint32_t L, uint32_t lp, uint32_t* wave_lds_floats, uint32_t* lds_stage_limit,
-                 uint64_t* scratch_floats, uint32_t* virt, uint32_t* v3, uint32_t* sb)
+#ifndef PCG_SCL_VIRT_DEFAULT
+#define PCG_SCL_VIRT_DEFAULT 2 // recomputed top stages (2: the quarters too, where sclls_layout allows)
+#endif
+int sclls_layout(uint32_t N, uint32_t L, uint32_t lp, bool quarters_ok, uint32_t* wave_lds_floats,
+                 uint32_t* lds_stage_limit, uint64_t* scratch_floats, uint32_t* virt, uint32_t* v3, uint32_t* sb)
 {
     const bool db = lp >= PCG_LS_DBITS_LP;
     if (L < 2 || L > 32 || N < 8)
@@ -2108,20 +2234,40 @@ int sclls_layout(uint32_t N, uint32_t L, uint32_t lp, uint32_t* wave_lds_floats,
         budget = bitsf + 2048u;
     if (const char* e = getenv("PCG_SCL_LDS_KB"))
         budget = (uint32_t)atoi(e) * 1024 / 4;
-    uint32_t vt = ls_max_virt(top);
+    // virt = 2 (quarters recomputed inside their staged F/G ops, ls_fgf_root2) needs the
+    // caller's guarantee that every node of stage >= top-2 is internal with both fusions on
+    // (quarters_ok), N >= 512 (8-chunk bit words), the quarters' grandchildren in the slab and
+    // the stage region of LDS holding one staging round (checked below, else virt = 1)
+    uint32_t vmax = ls_max_virt(top);
+    if (!quarters_ok || top < 9)
+        vmax = vmax < 1u ? vmax : 1u;
+    uint32_t vt = vmax < PCG_SCL_VIRT_DEFAULT ? vmax : PCG_SCL_VIRT_DEFAULT;
     if (const char* e = getenv("PCG_SCL_VIRT")) {
         const uint32_t v = (uint32_t)atoi(e);
-        vt = v < vt ? v : vt;
+        vt = v < vmax ? v : vmax;
+    }
+    auto stage_limit = [&](uint32_t mtv, uint32_t Sbv) {
+        uint32_t S = mtv;
+        while (S > LS_MINS && ls_layout(top, S, w3, Sbv).total > budget)
+            --S;
+        return S;
+    };
+    if (vt == 2) {
+        uint32_t Sb0 = top + 1 < 8u ? top + 1 : 8u;
+        Sb0 = !db ? 0u : (Sb0 < 5u ? 5u : Sb0);
+        const uint32_t S = stage_limit(ls_mtop(top, 2), Sb0), ab = ls_abase(w3);
+        const uint32_t region = (1u << S) > ab ? 4u * 64u * ((1u << S) - ab) : 0u;
+        const uint32_t mneed = lp / 16u > 1u ? lp / 16u : 1u;
+        if (S + 4u > top || (64u / lp) * 16u * mneed * 16u > region)
+            vt = 1;
     }
     const uint32_t mt = ls_mtop(top, vt);
     // LDS: the small D stages (4-7: every leaf and Combine writes one), then LLR stages up
     // from 3+v3, then the larger D stages while they fit
     uint32_t Sb = top + 1 < 8u ? top + 1 : 8u;
     Sb = !db ? 0u : (Sb < 5u ? 5u : Sb);
-    uint32_t Sl = mt;
-    while (Sl > LS_MINS && ls_layout(top, Sl, w3, Sb).total > budget)
-        --Sl;
-    if (const char* e = getenv("PCG_SCL_STAGE_LIMIT")) {
+    uint32_t Sl = stage_limit(mt, Sb);
+    if (const char* e = getenv("PCG_SCL_STAGE_LIMIT"); e && vt < 2) {
         const uint32_t v = (uint32_t)atoi(e);
         if (v >= LS_MINS && v <= mt)
             Sl = v;

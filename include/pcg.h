@@ -103,6 +103,9 @@ typedef struct pcg_plan_desc {
                                     wider); Fast-SSC scq kernel: its Q; 0 for the other kernels */
     uint32_t dev_overrides;      /* PCG_DEV_* bits: developer environment switches
                                     that changed this plan's kernel or layout; 0 in production */
+    uint32_t recomputed_stages;  /* lane-serial SCL: top LLR stages recomputed from the channel
+                                    where read instead of stored (1: the root's children, 2:
+                                    also its grandchildren); 0 for the other kernels */
 } pcg_plan_desc;
 
 #define PCG_DEV_SCL_LP 0x1   /* PCG_SCL_LP / PCG_ADAPT_LP (only when the caller passed 0) */
