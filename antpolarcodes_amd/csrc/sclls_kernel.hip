@@ -586,6 +586,12 @@ PCG_DEV void ls_fg(Src src, Dst dst, const DBits& lb, uint32_t s, const Share& w
     }
 }
 
+template <int OPC, bool R1, bool R2, bool FU, int LP, typename Dst2>
+PCG_DEV void ls_fgf_root2(const Ls<LP>& c, GlSt d1, Dst2 d2, const DBits& lb, const DBits& rb, const DBits& mb,
+                          uint32_t s, const Share& w, uint32_t m);
+template <int LP>
+PCG_DEV uint32_t ls_root_round(const Ls<LP>& c, uint32_t s, uint32_t h, bool fused);
+
 template <int OPC, int LP>
 PCG_DEV void ls_fg_op(Ls<LP>& c, uint32_t s, uint32_t o, uint32_t P)
 {
@@ -780,7 +786,7 @@ PCG_DEV void ls_fgf_root(const Ls<LP>& c, GlSt d1, Dst2 d2, const DBits& lb, con
 // Output chunks per staging round of ls_fgf_root, or 0 when it does not apply: the
 // LDS stages' region must hold a round, hold no output, and give every lane a chunk.
 template <int LP>
-PCG_DEV uint32_t ls_root_round(const Ls<LP>& c, uint32_t s, uint32_t h, bool fused = true)
+PCG_DEV uint32_t ls_root_round(const Ls<LP>& c, uint32_t s, uint32_t h, bool fused)
 {
     // (unfused: only the quarters' X, whose output alpha[s-1] must not be in the region)
     if (!c.stage_root || s != c.mt || s == c.top || s - (fused ? 2u : 1u) < c.Sl || (1u << c.Sl) <= c.ab)
@@ -883,7 +889,7 @@ PCG_DEV void ls_fgf_op(Ls<LP>& c, uint32_t s, uint32_t o, uint32_t P)
     const bool rootc = s >= c.mt && s != c.top, left = o < (c.N >> 1), quarter = rootc && s + 2u == c.top;
     const Share w = ls_share(c, P, s, quarter ? 0u : 1u << (s - 4)); // (quarters: one lane per path)
     const DBits lb = gbits(c, s, o, w.dl, w.bl);
-    const uint32_t rm = ls_root_round(c, s, w.h);
+    const uint32_t rm = ls_root_round(c, s, w.h, true);
     const DBits rb = rootc && !left && !quarter ? root_bits(c, w) : DBits{};
     auto run = [&](auto dst2) {
         GlSt d1 = gl_st(c, d);
