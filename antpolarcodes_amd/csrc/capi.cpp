@@ -82,19 +82,19 @@ int hip_fail(hipError_t e, const char* what)
     return fail(PCG_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
 
-// Every SCL node of stage >= top-2 internal (no leaf or size-8 subtree op there): the
-// condition for recomputing the quarters of the codeword inside their staged F/G ops
-// (sclls_layout, virt = 2).
-bool scl_top_nodes_internal(const std::vector<uint32_t>& ops, uint32_t top)
+// The largest V such that no SCL leaf or size-8 subtree op sits at stage >= top-V: the
+// recomputed top stages may go that deep (sclls_layout, virt = V).
+uint32_t scl_leaf_free_levels(const std::vector<uint32_t>& ops, uint32_t top)
 {
+    uint32_t hi = 0; // highest leaf stage
     for (size_t k = 0; k < ops.size(); ++k) {
         const uint32_t c = pcg::op_code(ops[k]), s = pcg::op_stage(ops[k]);
-        if (c >= pcg::OP_S_R0 && c <= pcg::OP_S_ST8 && s + 2u >= top)
-            return false;
+        if (c >= pcg::OP_S_R0 && c <= pcg::OP_S_ST8 && s > hi)
+            hi = s;
         if (c == pcg::OP_S_ST8)
             ++k; // its descriptor word
     }
-    return true;
+    return hi + 1u < top ? top - 1u - hi : 0u;
 }
 
 struct DeviceGuard {
@@ -343,8 +343,8 @@ static int plan_create_impl(pcg_plan** out,
             p->scl_fuse = (uint32_t)atoi(e);
             p->dev_overrides |= PCG_DEV_SCL_FUSE;
         }
-        const bool quarters_ok = (p->scl_fuse & 5u) == 5u && scl_top_nodes_internal(p->host.ops, p->host.log2N);
-        rc = pcg::sclls_layout(N, L, p->scl_lp, quarters_ok, &p->wave_lds_floats, &p->lds_stage_limit,
+        const uint32_t vleaf = (p->scl_fuse & 5u) == 5u ? scl_leaf_free_levels(p->host.ops, p->host.log2N) : 0u;
+        rc = pcg::sclls_layout(N, L, p->scl_lp, vleaf, &p->wave_lds_floats, &p->lds_stage_limit,
                                &p->scratch_floats, &p->scl_virt, &p->scl_v3, &p->scl_sb);
         if (rc != 0) {
             delete p;

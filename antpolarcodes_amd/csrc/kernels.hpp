@@ -102,7 +102,7 @@ inline uint64_t wave_units(uint64_t F, uint32_t frames_per_wave, uint64_t cap)
     return need < cap ? need : cap;
 }
 // lane-serial SCL kernel (sclls_kernel.hip), 64 / L' codewords per wave
-int sclls_layout(uint32_t N, uint32_t L, uint32_t lp, bool quarters_ok, uint32_t* wave_lds_floats,
+int sclls_layout(uint32_t N, uint32_t L, uint32_t lp, uint32_t vleaf, uint32_t* wave_lds_floats,
                  uint32_t* lds_stage_limit, uint64_t* scratch_floats, uint32_t* virt, uint32_t* v3, uint32_t* sb);
 uint64_t sclls_wave_cap(uint32_t lp, uint32_t wave_lds_floats);
 int launch_sclls(const KernelArgs& a, hipStream_t stream);

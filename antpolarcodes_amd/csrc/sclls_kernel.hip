@@ -76,7 +76,7 @@ __host__ __device__ inline uint32_t ls_mtop(uint32_t top, uint32_t virt)
     const uint32_t m = top - virt;
     return m > 3u ? m : 3u;
 }
-__host__ __device__ inline uint32_t ls_max_virt(uint32_t top) { return top >= 7 ? 2u : (top >= 4 ? 1u : 0u); }
+__host__ __device__ inline uint32_t ls_max_virt(uint32_t top) { return top >= 9 ? 2u : (top >= 4 ? 1u : 0u); }
 
 // Global scratch slab of one wave: alpha stages [Sl, mtop), then the tie-fallback
 // candidate list (64 * 8 values + 64 * 8 ids; rarely touched, so not worth LDS).
@@ -281,8 +281,8 @@ struct RootSt { // stage top-1, left or right child of the root
         return f4_g(a, b, lb.at(4u * c));
     }
 };
-// virt = 2: stage top-2 (the root's grandchildren, quarter q of the codeword) is recomputed
-// from four channel chunks, only inside the staged fused op (ls_fgf_root2).
+// virt = 2, 3: stages top-2 (the codeword's quarters) and top-3 (eighths, LP >= 16) are
+// recomputed from 4 / 8 channel chunks, only inside their staged F/G ops (ls_fgf_rootv).
 // Any recomputed stage behind one wave-uniform switch (leaves and size-8 subtrees at
 // stage top or top-1: rare, so one instantiation serves all of them).
 // (The left bits are read through the live context: a survivor's reload after ls_dup
@@ -518,15 +518,6 @@ PCG_DEV DBits root_bits(const Ls<LP>& c, const Share& w)
     else
         return rowbits(c, w.dl, 0u);
 }
-// the bits of the left child of the top-1 node holding the quarter at o (virt = 2)
-template <int LP>
-PCG_DEV DBits mid_bits(const Ls<LP>& c, const Share& w, uint32_t o)
-{
-    if constexpr (Ls<LP>::DB)
-        return dbits(c, c.top - 1u, w.shr ? path_dlane(c, w.dl, c.top - 1u) : c.dlane(c.top - 1u));
-    else
-        return rowbits(c, w.dl, o & ~((c.N >> 1) - 1u));
-}
 template <typename S>
 struct Off { // chunks [b, ...) of a storage
     S s;
@@ -586,9 +577,9 @@ PCG_DEV void ls_fg(Src src, Dst dst, const DBits& lb, uint32_t s, const Share& w
     }
 }
 
-template <int OPC, bool R1, bool R2, bool FU, int LP, typename Dst2>
-PCG_DEV void ls_fgf_root2(const Ls<LP>& c, GlSt d1, Dst2 d2, const DBits& lb, const DBits& rb, const DBits& mb,
-                          uint32_t s, const Share& w, uint32_t m);
+template <int OPC, bool FU, int LP>
+PCG_DEV void ls_rootv_op(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, uint32_t s, uint32_t o, const Share& w,
+                         uint32_t m);
 template <int LP>
 PCG_DEV uint32_t ls_root_round(const Ls<LP>& c, uint32_t s, uint32_t h, bool fused);
 
@@ -598,21 +589,15 @@ PCG_DEV void ls_fg_op(Ls<LP>& c, uint32_t s, uint32_t o, uint32_t P)
     const uint32_t d = s - 1;
     if (d >= c.mt || d < 3u + c.vlow) // recomputed where it is read
         return;
-    const bool quarter = s >= c.mt && s + 2u == c.top;
-    const Share w = ls_share(c, P, s, quarter ? 0u : 1u << (s - 3)); // (quarters: one lane per path)
+    const bool deep = s >= c.mt && s + 2u <= c.top; // a recomputed quarter / eighth
+    const Share w = ls_share(c, P, s, deep ? 0u : 1u << (s - 3)); // (those: one lane per path)
     const DBits lb = gbits(c, s, o, w.dl, w.bl);
-    if (quarter) { // a quarter whose child is a leaf: staged, unfused (alpha[s-1] is global)
+    if (deep) { // its child is a leaf: staged, unfused (alpha[s-1] is global)
         const uint32_t rm = ls_root_round(c, s, w.h, false);
-        if (rm) { // (always: sclls_layout plans virt = 2 only when it stages)
-            const DBits qr = root_bits(c, w), qm = mid_bits(c, w, o);
+        if (rm) { // (always: sclls_layout plans virt >= 2 only when it stages)
             GlSt d1 = gl_st(c, d);
             d1.lane = w.dl;
-            switch (o / (c.N >> 2)) {
-            case 0: ls_fgf_root2<OPC, false, false, false, LP>(c, d1, d1, lb, qr, qm, s, w, rm); break;
-            case 1: ls_fgf_root2<OPC, false, true, false, LP>(c, d1, d1, lb, qr, qm, s, w, rm); break;
-            case 2: ls_fgf_root2<OPC, true, false, false, LP>(c, d1, d1, lb, qr, qm, s, w, rm); break;
-            default: ls_fgf_root2<OPC, true, true, false, LP>(c, d1, d1, lb, qr, qm, s, w, rm); break;
-            }
+            ls_rootv_op<OPC, false, LP>(c, d1, d1, lb, s, o, w, rm);
         }
         c.own(d);
         return;
@@ -788,11 +773,13 @@ PCG_DEV void ls_fgf_root(const Ls<LP>& c, GlSt d1, Dst2 d2, const DBits& lb, con
 template <int LP>
 PCG_DEV uint32_t ls_root_round(const Ls<LP>& c, uint32_t s, uint32_t h, bool fused)
 {
-    // (unfused: only the quarters' X, whose output alpha[s-1] must not be in the region)
+    // (unfused: only a recomputed quarter's / eighth's X, whose output alpha[s-1] must not
+    // be in the region)
     if (!c.stage_root || s != c.mt || s == c.top || s - (fused ? 2u : 1u) < c.Sl || (1u << c.Sl) <= c.ab)
         return 0;
     const uint32_t region = 4u * 64u * ((1u << c.Sl) - c.ab); // bytes
-    const uint32_t k = s + 2u == c.top ? (fused ? 16u : 8u) : 8u; // channel chunks per output chunk
+    const uint32_t V = c.top - s;                                 // 1: a root child
+    const uint32_t k = V == 1 ? 8u : (fused ? 4u : 2u) << V;      // channel chunks per output chunk
     uint32_t m = fused ? 1u << (s - 4) : 1u << (s - 3);          // output chunks of the op
     while (m > 1 && (64u / LP) * k * m * 16u > region)
         m >>= 1;
@@ -800,37 +787,54 @@ PCG_DEV uint32_t ls_root_round(const Ls<LP>& c, uint32_t s, uint32_t h, bool fus
     return (64u / LP) * k * m * 16u <= region && m >= need && m >= 1 ? m : 0u;
 }
 
-// virt = 2: the fused op on a quarter (s = top-2), staged like ls_fgf_root with 16 channel
-// chunks per output chunk -- alpha[s] chunk a_k (k < 4: c2, c2+hq, c2+hq2, c2+hq2+hq) from
-// the channel chunks a_k + {0, N/8, N/16, N/16+N/8} at staged index 16u + 4k + j.  Bits: the
-// root's left half (R1), the top-1 node's left child (R2), the op's own G bits.
-// FU = false: the X alone (its child is a leaf): output chunk c2 < hq of alpha[s-1] from
-// alpha[s] chunks c2, c2+hq (8 staged chunks each, 4k + j, k < 2).
-template <int OPC, bool R1, bool R2, bool FU, int LP, typename Dst2>
-PCG_DEV void ls_fgf_root2(const Ls<LP>& c, GlSt d1, Dst2 d2, const DBits& lb, const DBits& rb, const DBits& mb,
-                          uint32_t s, const Share& w, uint32_t m)
+// virt >= 2: an F/G on a node of stage s = top-V (V = 2: a quarter of the codeword, 3: an
+// eighth), staged like ls_fgf_root.  Alpha[s] chunk a_k (k < KS: c2, c2+hq, and, fused with
+// the child's F, c2+hq2, c2+hq2+hq) is rebuilt from the 2^V channel chunks a_k + off(j),
+// off(j) = sum over the set bits l-1 of j of h_l = N/2^(l+2) chunks, staged at index
+// (u*KS + k)*2^V + j.  Level l = 1..V combines pairs along h_l: F, or G (RM bit l-1) with
+// the bits of the left child of the level-l ancestor -- vb[l-1]: the root's left half, then
+// D[top-1] / the row at that node, D[top-2] / ...  FU = false: the X alone (its child is a
+// leaf): output chunk c2 < hq of alpha[s-1] from alpha[s] chunks c2, c2+hq.
+template <int OPC, int V, int RM, bool FU, int LP>
+PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, const DBits (&vb)[3], uint32_t s,
+                          const Share& w, uint32_t m)
 {
-    constexpr uint32_t KS = FU ? 4u : 2u; // alpha[s] chunks per output chunk
-    const uint32_t hq = 1u << (s - 3), hq2 = hq >> 1, h8 = c.N >> 3, h16 = c.N >> 4;
-    const uint32_t nout = FU ? hq2 : hq;  // output chunks of the op
+    constexpr uint32_t KS = FU ? 4u : 2u, J = 1u << V;
+    const uint32_t hq = 1u << (s - 3), hq2 = hq >> 1;
+    const uint32_t hl[3] = { c.N >> 3, c.N >> 4, c.N >> 5 };
+    const uint32_t nout = FU ? hq2 : hq;           // output chunks of the op
     float* stg = c.lds + c.ly.alpha;
-    const uint32_t per = 4u * KS * m;              // chunks per codeword per round
+    const uint32_t per = KS * J * m;               // chunks per codeword per round
     const uint32_t ninst = (64u / LP) * per / 64u; // DMA instructions per round
     const uint32_t n = m / w.h;                    // output chunks per lane per round
     const uint64_t yp = (uint64_t)(uintptr_t)c.y;
     const float4* mine = reinterpret_cast<const float4*>(stg) + (c.lane / LP) * per;
-    // bit words of 8 aligned output chunks (s >= 7, N >= 128: every offset a multiple of 8)
-    uint32_t rw[4][2] = { { 0, 0 }, { 0, 0 }, { 0, 0 }, { 0, 0 } }, mw[4] = { 0, 0, 0, 0 }, lw[2] = { 0, 0 };
+    auto koff = [&](uint32_t k) { return ((k & 1u) ? hq : 0u) + ((k & 2u) ? hq2 : 0u); };
+    // bit words of 8 aligned output chunks (s >= 7: every offset a multiple of 8 chunks):
+    // level l's J >> l outputs at bw[k][J - (J >> (l-1)) + i]
+    uint32_t bw[KS][J], lw[2] = { 0, 0 };
+#pragma unroll
+    for (uint32_t k = 0; k < KS; ++k)
+#pragma unroll
+        for (uint32_t i = 0; i < J; ++i)
+            bw[k][i] = 0;
     auto words = [&](uint32_t cg) {
 #pragma unroll
         for (uint32_t k = 0; k < KS; ++k) {
-            const uint32_t a = cg + ((k & 1) ? hq : 0u) + ((k & 2) ? hq2 : 0u);
-            if (R1) {
-                rw[k][0] = rb.wat(4u * a);
-                rw[k][1] = rb.wat(4u * (a + h16));
+            const uint32_t a = cg + koff(k);
+#pragma unroll
+            for (int l = 1; l <= V; ++l) {
+                if (!((RM >> (l - 1)) & 1))
+                    continue;
+#pragma unroll
+                for (uint32_t i = 0; i < (J >> l); ++i) {
+                    uint32_t off = 0;
+#pragma unroll
+                    for (int q = l + 1; q <= V; ++q)
+                        off += ((i >> (q - l - 1)) & 1u) ? hl[q - 1] : 0u;
+                    bw[k][J - (J >> (l - 1)) + i] = vb[l - 1].wat(4u * (a + off));
+                }
             }
-            if (R2)
-                mw[k] = mb.wat(4u * a);
         }
         if (OPC == OP_G) {
             lw[0] = lb.wat(4u * cg);
@@ -843,9 +847,11 @@ PCG_DEV void ls_fgf_root2(const Ls<LP>& c, GlSt d1, Dst2 d2, const DBits& lb, co
         __builtin_amdgcn_wave_barrier();
         for (uint32_t t = 0; t < ninst; ++t) {
             const uint32_t f = t * 64u + c.lane;
-            const uint32_t g = f / per, rem = f % per, u = rem / (4u * KS), k = (rem >> 2) % KS, j = rem & 3u;
-            uint32_t a = r + u + ((k & 1u) ? hq : 0u) + ((k & 2u) ? hq2 : 0u);
-            a += ((j & 1u) ? h8 : 0u) + ((j & 2u) ? h16 : 0u);
+            const uint32_t g = f / per, rem = f % per, u = rem / (KS * J), k = (rem / J) % KS, j = rem % J;
+            uint32_t a = r + u + koff(k);
+#pragma unroll
+            for (int l = 1; l <= V; ++l)
+                a += ((j >> (l - 1)) & 1u) ? hl[l - 1] : 0u;
             const uint32_t lo = shfl((uint32_t)yp, (int)(g * LP)), hi = shfl((uint32_t)(yp >> 32), (int)(g * LP));
             const float* src = reinterpret_cast<const float*>((uintptr_t)(((uint64_t)hi << 32) | lo)) + 4u * a;
             __builtin_amdgcn_global_load_lds(src, stg + t * 256u, 16, 0, 0);
@@ -864,11 +870,17 @@ PCG_DEV void ls_fgf_root2(const Ls<LP>& c, GlSt d1, Dst2 d2, const DBits& lb, co
             float4 x[KS];
 #pragma unroll
             for (uint32_t k = 0; k < KS; ++k) {
-                const uint32_t b = u * 4u * KS + 4u * k;
-                const float4 y0 = mine[b], y1 = mine[b + 1u], y2 = mine[b + 2u], y3 = mine[b + 3u];
-                const float4 b0 = R1 ? f4_g(y0, y1, rw[k][0] >> gs) : f4_f(y0, y1);
-                const float4 b1 = R1 ? f4_g(y2, y3, rw[k][1] >> gs) : f4_f(y2, y3);
-                x[k] = R2 ? f4_g(b0, b1, mw[k] >> gs) : f4_f(b0, b1);
+                float4 v[J];
+#pragma unroll
+                for (uint32_t j = 0; j < J; ++j)
+                    v[j] = mine[(u * KS + k) * J + j];
+#pragma unroll
+                for (int l = 1; l <= V; ++l)
+#pragma unroll
+                    for (uint32_t i = 0; i < (J >> l); ++i)
+                        v[i] = ((RM >> (l - 1)) & 1) ? f4_g(v[2 * i], v[2 * i + 1], bw[k][J - (J >> (l - 1)) + i] >> gs)
+                                                     : f4_f(v[2 * i], v[2 * i + 1]);
+                x[k] = v[0];
             }
             const float4 y0 = OPC == OP_F ? f4_f(x[0], x[1]) : f4_g(x[0], x[1], lw[0] >> gs);
             d1.st(c2, y0);
@@ -882,31 +894,83 @@ PCG_DEV void ls_fgf_root2(const Ls<LP>& c, GlSt d1, Dst2 d2, const DBits& lb, co
     __builtin_amdgcn_s_waitcnt(0);
 }
 
+// the bits level l of a recomputed stage-(top-V) node at o reads: the left child of its
+// level-l ancestor (l = 1: the root's left half; 2: D[top-1] / the row at the top-1 node;
+// 3: D[top-2] / the row at the top-2 node) for the path in lane w.dl
+template <int LP>
+PCG_DEV void level_bits(const Ls<LP>& c, const Share& w, uint32_t o, DBits (&vb)[3])
+{
+    vb[0] = root_bits(c, w);
+#pragma unroll
+    for (uint32_t l = 2; l <= 3; ++l) {
+        const uint32_t st = c.top + 1u - l;
+        if constexpr (Ls<LP>::DB)
+            vb[l - 1] = dbits(c, st, w.shr ? path_dlane(c, w.dl, st) : c.dlane(st));
+        else
+            vb[l - 1] = rowbits(c, w.dl, o & ~((1u << st) - 1u));
+    }
+}
+// Run the staged op on the recomputed node of stage s = top-V at o (V = 2, or 3 for LP >= 16)
+template <int OPC, bool FU, int LP>
+PCG_DEV void ls_rootv_op(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, uint32_t s, uint32_t o, const Share& w,
+                         uint32_t m)
+{
+    DBits vb[3];
+    level_bits(c, w, o, vb);
+    const uint32_t V = c.top - s;
+    // RM bit l-1: the level-l ancestor's right child holds the node
+    uint32_t rm = 0;
+    for (uint32_t l = 1; l <= V; ++l)
+        rm |= ((o >> (c.top - l)) & 1u) << (l - 1);
+    if (V == 2) {
+        switch (rm) {
+        case 0: ls_fgf_rootv<OPC, 2, 0, FU, LP>(c, d1, d2, lb, vb, s, w, m); break;
+        case 1: ls_fgf_rootv<OPC, 2, 1, FU, LP>(c, d1, d2, lb, vb, s, w, m); break;
+        case 2: ls_fgf_rootv<OPC, 2, 2, FU, LP>(c, d1, d2, lb, vb, s, w, m); break;
+        default: ls_fgf_rootv<OPC, 2, 3, FU, LP>(c, d1, d2, lb, vb, s, w, m); break;
+        }
+        return;
+    }
+    if constexpr (LP >= 16) {
+        switch (rm) {
+        case 0: ls_fgf_rootv<OPC, 3, 0, FU, LP>(c, d1, d2, lb, vb, s, w, m); break;
+        case 1: ls_fgf_rootv<OPC, 3, 1, FU, LP>(c, d1, d2, lb, vb, s, w, m); break;
+        case 2: ls_fgf_rootv<OPC, 3, 2, FU, LP>(c, d1, d2, lb, vb, s, w, m); break;
+        case 3: ls_fgf_rootv<OPC, 3, 3, FU, LP>(c, d1, d2, lb, vb, s, w, m); break;
+        case 4: ls_fgf_rootv<OPC, 3, 4, FU, LP>(c, d1, d2, lb, vb, s, w, m); break;
+        case 5: ls_fgf_rootv<OPC, 3, 5, FU, LP>(c, d1, d2, lb, vb, s, w, m); break;
+        case 6: ls_fgf_rootv<OPC, 3, 6, FU, LP>(c, d1, d2, lb, vb, s, w, m); break;
+        default: ls_fgf_rootv<OPC, 3, 7, FU, LP>(c, d1, d2, lb, vb, s, w, m); break;
+        }
+    }
+}
+
 template <int OPC, int LP>
 PCG_DEV void ls_fgf_op(Ls<LP>& c, uint32_t s, uint32_t o, uint32_t P)
 {
     const uint32_t d = s - 1, e = s - 2;
-    const bool rootc = s >= c.mt && s != c.top, left = o < (c.N >> 1), quarter = rootc && s + 2u == c.top;
-    const Share w = ls_share(c, P, s, quarter ? 0u : 1u << (s - 4)); // (quarters: one lane per path)
+    const bool rootc = s >= c.mt && s != c.top, left = o < (c.N >> 1), deep = rootc && s + 2u <= c.top;
+    const Share w = ls_share(c, P, s, deep ? 0u : 1u << (s - 4)); // (quarters / eighths: one lane per path)
     const DBits lb = gbits(c, s, o, w.dl, w.bl);
     const uint32_t rm = ls_root_round(c, s, w.h, true);
-    const DBits rb = rootc && !left && !quarter ? root_bits(c, w) : DBits{};
+    if (deep) { // a recomputed quarter / eighth: staged (its grandchild alpha[s-2] is global)
+        if (rm) { // (always: sclls_layout plans virt >= 2 only when it stages)
+            GlSt d1 = gl_st(c, d), d2 = gl_st(c, e);
+            d1.lane = w.dl;
+            d2.lane = w.dl;
+            ls_rootv_op<OPC, true, LP>(c, d1, d2, lb, s, o, w, rm);
+        }
+        c.own(d);
+        c.own(e);
+        return;
+    }
+    const DBits rb = rootc && !left ? root_bits(c, w) : DBits{};
     auto run = [&](auto dst2) {
         GlSt d1 = gl_st(c, d);
         d1.lane = w.dl;
         dst2.lane = w.dl;
         if (s == c.top) {
             ls_fgf<OPC, LP>(ChSt{ c.y }, d1, dst2, lb, s, w);
-        } else if (quarter && rm) {
-            const DBits qr = root_bits(c, w), qm = mid_bits(c, w, o);
-            switch (o / (c.N >> 2)) {
-            case 0: ls_fgf_root2<OPC, false, false, true, LP>(c, d1, dst2, lb, qr, qm, s, w, rm); break;
-            case 1: ls_fgf_root2<OPC, false, true, true, LP>(c, d1, dst2, lb, qr, qm, s, w, rm); break;
-            case 2: ls_fgf_root2<OPC, true, false, true, LP>(c, d1, dst2, lb, qr, qm, s, w, rm); break;
-            default: ls_fgf_root2<OPC, true, true, true, LP>(c, d1, dst2, lb, qr, qm, s, w, rm); break;
-            }
-        } else if (quarter) {
-            return; // (unreachable: sclls_layout plans virt = 2 only when this op stages)
         } else if (rm && left)
             ls_fgf_root<OPC, true, LP>(c, d1, dst2, lb, rb, s, w, rm);
         else if (rm)
@@ -918,7 +982,6 @@ PCG_DEV void ls_fgf_op(Ls<LP>& c, uint32_t s, uint32_t o, uint32_t P)
         else
             ls_fgf<OPC, LP>(gl_st(c, s), d1, dst2, lb, s, w);
     };
-    (void)quarter;
     if (e >= c.Sl)
         run(gl_st(c, e));
     else
@@ -2213,9 +2276,9 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
 } // namespace
 
 #ifndef PCG_SCL_VIRT_DEFAULT
-#define PCG_SCL_VIRT_DEFAULT 2 // recomputed top stages (2: the quarters too, where sclls_layout allows)
+#define PCG_SCL_VIRT_DEFAULT 3 // recomputed top stages (2: the quarters too, 3: eighths for LP >= 16, where sclls_layout allows)
 #endif
-int sclls_layout(uint32_t N, uint32_t L, uint32_t lp, bool quarters_ok, uint32_t* wave_lds_floats,
+int sclls_layout(uint32_t N, uint32_t L, uint32_t lp, uint32_t vleaf, uint32_t* wave_lds_floats,
                  uint32_t* lds_stage_limit, uint64_t* scratch_floats, uint32_t* virt, uint32_t* v3, uint32_t* sb)
 {
     const bool db = lp >= PCG_LS_DBITS_LP;
@@ -2240,13 +2303,16 @@ int sclls_layout(uint32_t N, uint32_t L, uint32_t lp, bool quarters_ok, uint32_t
         budget = bitsf + 2048u;
     if (const char* e = getenv("PCG_SCL_LDS_KB"))
         budget = (uint32_t)atoi(e) * 1024 / 4;
-    // virt = 2 (quarters recomputed inside their staged F/G ops, ls_fgf_root2) needs the
-    // caller's guarantee that every node of stage >= top-2 is internal with both fusions on
-    // (quarters_ok), N >= 512 (8-chunk bit words), the quarters' grandchildren in the slab and
-    // the stage region of LDS holding one staging round (checked below, else virt = 1)
+    // virt = V >= 2 (stages top-1 .. top-V recomputed, the deepest inside its staged F/G ops,
+    // ls_fgf_rootv) needs: no leaf at stage >= top-V with both fusions on (the caller's vleaf
+    // >= V), V = 3 only for LP >= 16, stage top-V >= 7 (8-chunk bit words), the recomputed
+    // nodes' grandchildren in the slab and the LDS stage region holding one staging round
+    // (checked below, else one level less)
     uint32_t vmax = ls_max_virt(top);
-    if (!quarters_ok || top < 9)
-        vmax = vmax < 1u ? vmax : 1u;
+    if (lp >= 16 && top >= 10 && vleaf >= 3)
+        vmax = 3;
+    while (vmax >= 2 && (vleaf < vmax || top < 7 + vmax))
+        --vmax;
     uint32_t vt = vmax < PCG_SCL_VIRT_DEFAULT ? vmax : PCG_SCL_VIRT_DEFAULT;
     if (const char* e = getenv("PCG_SCL_VIRT")) {
         const uint32_t v = (uint32_t)atoi(e);
@@ -2258,14 +2324,16 @@ int sclls_layout(uint32_t N, uint32_t L, uint32_t lp, bool quarters_ok, uint32_t
             --S;
         return S;
     };
-    if (vt == 2) {
+    while (vt >= 2) {
         uint32_t Sb0 = top + 1 < 8u ? top + 1 : 8u;
         Sb0 = !db ? 0u : (Sb0 < 5u ? 5u : Sb0);
-        const uint32_t S = stage_limit(ls_mtop(top, 2), Sb0), ab = ls_abase(w3);
+        const uint32_t S = stage_limit(ls_mtop(top, vt), Sb0), ab = ls_abase(w3);
         const uint32_t region = (1u << S) > ab ? 4u * 64u * ((1u << S) - ab) : 0u;
-        const uint32_t mneed = lp / 16u > 1u ? lp / 16u : 1u;
-        if (S + 4u > top || (64u / lp) * 16u * mneed * 16u > region)
-            vt = 1;
+        const uint32_t kc = 4u << vt; // staged channel chunks per output chunk (fused)
+        const uint32_t mneed = lp / kc > 1u ? lp / kc : 1u;
+        if (S + vt + 2u <= top && (64u / lp) * kc * mneed * 16u <= region)
+            break;
+        --vt;
     }
     const uint32_t mt = ls_mtop(top, vt);
     // LDS: the small D stages (4-7: every leaf and Combine writes one), then LLR stages up

@@ -61,14 +61,14 @@ def test_scl_random_frozen_sets(oracle):
         _check_scl(oracle, N, L, fr, llr, crc=0)
 
 
-@pytest.mark.parametrize("virt", [1, 2])
+@pytest.mark.parametrize("virt", [1, 2, 3])
 @pytest.mark.parametrize("L", [2, 8, 16, 32])
 def test_scl_recomputed_top_stages(oracle, monkeypatch, virt, L):
     """The top LLR stages recomputed from the channel where read (sclls layout):
     virt 1 = the root's children, 2 = also its grandchildren (the codeword's quarters),
-    the default where every node of stage >= top-2 is internal.  Both against the oracle,
-    systematic and not, with the quarters' F/G fused (N = 2048) and unfused (leaf children,
-    BB(1024, 512))."""
+    3 = also the eighths (LP >= 16); the deepest allowed by the leaves is the default.  All
+    against the oracle, systematic and not, with the deepest nodes' F/G fused (N = 2048) and
+    unfused (leaf children, BB(1024, 512))."""
     from antpolarcodes_amd import frames
     monkeypatch.setenv("PCG_SCL_VIRT", str(virt))
     rng = np.random.default_rng(31 * L + virt)
@@ -76,7 +76,11 @@ def test_scl_recomputed_top_stages(oracle, monkeypatch, virt, L):
         fr = oracle.frozen_bits_bb(N, K, 0.0)
         p = _plan(N, L, fr)
         got = p.describe()["recomputed_stages"]
-        assert got in (1, virt) and (virt == 1 or N != 1024 or got == 2), got
+        assert 1 <= got <= virt, got
+        if N == 1024 and virt >= 2:
+            assert got == 2, got  # BB(1024, 512) has leaves at stage 7: the quarters, not the eighths
+        if N == 2048 and virt == 3 and L >= 16:
+            assert got == 3, got
         for kind in LLR_KINDS[:4]:
             _check_scl(oracle, N, L, fr, llr_kinds(rng, 4, N, kind))
         llr, _, _ = frames.awgn_frames(N, fr, 64, 1.5, seed=N + L, crc=8, systematic=False)
