@@ -256,7 +256,8 @@ static int plan_create_impl(pcg_plan** out,
                             int crc_kind,
                             int device,
                             int fixed,
-                            uint32_t scl_lp = 0)
+                            uint32_t scl_lp = 0,
+                            bool walk_latency = false)
 {
     if (!out)
         return fail(PCG_E_ARG, "plan output pointer is null");
@@ -343,7 +344,12 @@ static int plan_create_impl(pcg_plan** out,
             p->scl_fuse = (uint32_t)atoi(e);
             p->dev_overrides |= PCG_DEV_SCL_FUSE;
         }
-        const uint32_t vleaf = (p->scl_fuse & 5u) == 5u ? scl_leaf_free_levels(p->host.ops, p->host.log2N) : 0u;
+        // (an adaptive plan's list stage is one walk over a few frames: its latency, not its
+        // traffic, counts -- the root's children only: 6.18e7 vs 5.99e7 cw/s for AdaptiveFloat
+        // L = 8, profiles/r03p_adaptive_virt_sweep.txt)
+        const uint32_t vleaf = (p->scl_fuse & 5u) == 5u && !walk_latency
+                                   ? scl_leaf_free_levels(p->host.ops, p->host.log2N)
+                                   : 0u;
         rc = pcg::sclls_layout(N, L, p->scl_lp, vleaf, &p->wave_lds_floats, &p->lds_stage_limit,
                                &p->scratch_floats, &p->scl_virt, &p->scl_v3, &p->scl_sb);
         if (rc != 0) {
@@ -485,7 +491,7 @@ static int plan_create_adaptive_impl(pcg_plan** out,
     const char* lpe = getenv("PCG_ADAPT_LP");
     if (lpe)
         lp = (uint32_t)strtoul(lpe, nullptr, 10);
-    int rc = plan_create_impl(out, N, L, frozen, n_frozen, systematic, crc_kind, device, fixed, fixed ? 0 : lp);
+    int rc = plan_create_impl(out, N, L, frozen, n_frozen, systematic, crc_kind, device, fixed, fixed ? 0 : lp, true);
     if (rc != 0)
         return rc;
     if (lpe)

@@ -55,6 +55,44 @@ PCG_DEV uint32_t q_sgn4(const float4& v)
 }
 PCG_DEV float q_at(const float4& v, uint32_t k) { return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w)); }
 
+// Lane J of this lane's codeword group.  Q = 16: the group is one DPP row, so the broadcast
+// is a row_newbcast move (VALU, no LDS crossbar round trip); other Q: ds_bpermute.
+template <int Q, int J>
+PCG_DEV uint32_t gbc(uint32_t v, int base)
+{
+    if constexpr (Q == 16)
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + J, 0xF, 0xF, false);
+    else
+        return (uint32_t)__shfl((int)v, base + J, 64);
+}
+// o[j] = lane j of the group, j < N
+template <int Q, int N, int J = 0>
+PCG_DEV void gbc_all(uint32_t v, int base, uint32_t (&o)[N])
+{
+    if constexpr (J < N) {
+        o[J] = gbc<Q, J>(v, base);
+        gbc_all<Q, N, J + 1>(v, base, o);
+    }
+}
+template <int Q, int N>
+PCG_DEV void gbc_allf(float v, int base, float (&o)[N])
+{
+    uint32_t u[N];
+    gbc_all<Q, N>(fbits(v), base, u);
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+        o[j] = ubits(u[j]);
+}
+// lane i ^ 8 of the group (Q = 16: row_ror:8)
+template <int Q>
+PCG_DEV float gxor8(float v, int base, uint32_t i)
+{
+    if constexpr (Q == 16)
+        return ubits((uint32_t)__builtin_amdgcn_update_dpp(0, (int)fbits(v), 0x128, 0xF, 0xF, false));
+    else
+        return __shfl(v, base + (int)(i ^ 8u), 64);
+}
+
 // OR of a value over aligned groups of 8 lanes (exact xor partners 1, 2, 4)
 PCG_DEV uint32_t or8(uint32_t v)
 {
@@ -436,9 +474,7 @@ PCG_DEV void grp_lane_sums(const Cw<Q>& w, const SRC& src, uint32_t n, float (&s
                 acc = acc + src.at(i);
     }
     const int base = (int)(__lane_id() & ~(uint32_t)(Q - 1));
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-        s[j] = __shfl(acc, base + j, 64);
+    gbc_allf<Q, 8>(acc, base, s);
 }
 
 // positions [o, o+n) := periodic pattern, every lane holding the same `pat`
@@ -523,13 +559,14 @@ PCG_DEV bool grp_leaf(const Cw<Q>& w, uint32_t code, const SRC& src, uint32_t n,
             }
         const int base = (int)(__lane_id() & ~(uint32_t)(Q - 1));
         float mv[8];
-        uint32_t mi[8];
+        uint32_t mi[8], pjs[8];
         uint32_t pe = 0, po = 0;
+        gbc_allf<Q, 8>(mvj, base, mv);
+        gbc_all<Q, 8>(mij, base, mi);
+        gbc_all<Q, 8>(pjj, base, pjs);
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            mv[j] = __shfl(mvj, base + j, 64);
-            mi[j] = __shfl(mij, base + j, 64);
-            const uint32_t pj = __shfl(pjj, base + j, 64);
+            const uint32_t pj = pjs[j];
             if (j & 1)
                 po ^= pj;
             else
@@ -618,10 +655,12 @@ PCG_DEV void leaf_body(const Cw<Q>& w, uint32_t code, const SRC& src, uint32_t s
             for (uint32_t i = w.sub; i < n; i += 8)
                 acc = acc + src.at(i);
         const uint32_t base = __lane_id() & ~(uint32_t)(Q - 1);
-        float S = __shfl(acc, (int)base, 64);
+        float t[8];
+        gbc_allf<Q, 8>(acc, (int)base, t);
+        float S = t[0];
 #pragma unroll
         for (int j = 1; j < 8; ++j)
-            S = S + __shfl(acc, (int)base + j, 64);
+            S = S + t[j];
         w.fill(o, n, (fbits(S) >> 31) ? 0xffffffffu : 0u);
         return;
     }
@@ -973,9 +1012,7 @@ PCG_DEV void q16_par(const Cw<Q>& w, uint32_t code, uint32_t o, uint32_t desc)
         x = right ? polar_g(p0, p1, lb << 31) : polar_f(p0, p1);
         if ((desc >> 17) & 1u) { // a size-16 leaf child
             float xs[16];
-#pragma unroll
-            for (int j = 0; j < 16; ++j)
-                xs[j] = __shfl(x, base + j, 64);
+            gbc_allf<Q, 16>(x, base, xs);
             const uint32_t bits = leaf16_bits(desc & 0xffu, xs);
             if (w.sub == 0)
                 w.put(o, 16, bits);
@@ -985,20 +1022,16 @@ PCG_DEV void q16_par(const Cw<Q>& w, uint32_t code, uint32_t o, uint32_t desc)
         x = w.psrc(4).at(i);
     }
     const bool rone = code == OP_Q16R || ((code == OP_Q16F || code == OP_Q16G) && ((desc >> 16) & 1u));
-    const float xu = __shfl(x, base + (int)(i ^ 8u), 64); // element i + 8 on lanes i < 8
+    const float xu = gxor8<Q>(x, base, i); // element i + 8 on lanes i < 8
     const float lf = polar_f(x, xu);
     float l[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-        l[j] = __shfl(lf, base + j, 64);
+    gbc_allf<Q, 8>(lf, base, l);
     const uint32_t bl = leaf8_bits(desc & 0xffu, l);
     const float rg = polar_g(x, xu, ((bl >> (i & 7u)) & 1u) << 31);
     uint32_t br;
     if (!rone) {
         float r[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            r[j] = __shfl(rg, base + j, 64);
+        gbc_allf<Q, 8>(rg, base, r);
         br = leaf8_bits((desc >> 8) & 0xffu, r);
     } else { // right rate-1: the signs of r (lanes 0..7 of the group)
         br = (uint32_t)(__ballot(sgn(rg) != 0) >> base) & 0xffu;
