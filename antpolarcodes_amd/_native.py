@@ -41,6 +41,7 @@ class PlanDesc(C.Structure):
         ("lanes_per_codeword", C.c_uint32),
         ("dev_overrides", C.c_uint32),  # PCG_DEV_* bits: non-default kernel/layout from dev env switches
         ("recomputed_stages", C.c_uint32),  # lane-serial SCL: top stages recomputed (1 or 2)
+        ("specialized", C.c_uint32),  # 1: decodes run the plan-specialised kernel (pcg_plan_specialize)
     ]
 
 
@@ -87,6 +88,7 @@ def lib():
         L.pcg_plan_kernel_name.argtypes = [P]
         L.pcg_plan_kernel_name.restype = C.c_char_p
         L.pcg_plan_set_initial_metric.argtypes = [P, C.c_float]
+        L.pcg_plan_specialize.argtypes = [P]
         L.pcg_plan_destroy.argtypes = [P]
         L.pcg_plan_destroy.restype = None
         L.pcg_last_error.restype = C.c_char_p
@@ -178,6 +180,11 @@ class Plan:
     def kernel_name(self):
         """The decode kernel as rocprofv3 names it (pcg_plan_kernel_name)."""
         return lib().pcg_plan_kernel_name(self._h).decode()
+
+    def specialize(self):
+        """Compile and load the kernel specialised to this plan's code (pcg_plan_specialize,
+        hiprtc; Fast-SSC float plans).  Raises PcgError if that fails or is unsupported."""
+        _check(lib().pcg_plan_specialize(self._h))
 
     def set_initial_metric(self, m):
         """SCL: initial path-0 metric of later decodes (reference metric carry)."""

@@ -4,11 +4,14 @@
 #include "frames.hpp"
 #include "kernels.hpp"
 #include "plan.hpp"
+#include "rtc.hpp"
 
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
+#include <future>
 #include <string>
 #include <vector>
 
@@ -64,6 +67,17 @@ struct pcg_plan {
     hipStream_t last_stream = nullptr;
     bool has_last = false;
     uint32_t dev_overrides = 0;   // PCG_DEV_* bits: developer switches that changed this plan
+    // plan-specialised kernel (rtc.cpp; Fast-SSC float plans on the scq kernel): rtc_mode 0 =
+    // never, 1 = compile at the first decode and wait for it, 2 = compile in the background
+    // from the first decode of >= RTC_AUTO_FRAMES frames, switching once it is ready
+    // (PCG_RTC=0/1, default 2); rtc_state 0 = not tried, 2 = compiling (rtc_job), 1 = loaded,
+    // -1 = failed (rtc_err)
+    int rtc_mode = 2;
+    int rtc_state = 0;
+    std::future<std::pair<std::vector<char>, std::string>> rtc_job;
+    std::string rtc_err;
+    hipModule_t rtc_mod = nullptr;
+    hipFunction_t rtc_fn = nullptr;
 };
 
 namespace {
@@ -137,6 +151,69 @@ void free_plan_device(pcg_plan* p)
     (void)hipFree(p->d_dep);
     (void)hipFree(p->d_fmap);
     (void)hipFree(p->d_okbuf);
+    if (p->rtc_mod)
+        (void)hipModuleUnload(p->rtc_mod);
+    p->rtc_mod = nullptr;
+    p->rtc_fn = nullptr;
+}
+
+// Batches from this size on specialise a Fast-SSC plan's kernel at their first decode (the
+// hiprtc compile takes seconds once per code and process; smaller batches are latency work).
+constexpr uint64_t RTC_AUTO_FRAMES = 8192;
+
+bool rtc_capable(const pcg_plan* p)
+{
+    return !p->host.fixed && p->host.L == 1 && p->host.sc_kind == 2 && !p->dev_opprof;
+}
+
+// Compile (hiprtc, cached per process and on disk) and, on a device plan, load the plan's
+// specialised kernel -- or, with wait = false, start the compile in the background and load
+// it at a later call once it has finished; on failure the plan keeps the interpreter kernel
+// and remembers why.
+int specialize(pcg_plan* p, bool wait = true)
+{
+    if (p->rtc_state == 1)
+        return PCG_OK;
+    if (p->rtc_state == -1)
+        return fail(PCG_E_HIP, p->rtc_err);
+    if (p->rtc_state == 0) {
+        pcg::PlanHost host = p->host; // the job's own copy
+        p->rtc_job = std::async(std::launch::async, [host] {
+            std::pair<std::vector<char>, std::string> r;
+            if (pcg::scq_rtc_compile(host, &r.first, &r.second) != 0)
+                r.first.clear();
+            return r;
+        });
+        p->rtc_state = 2;
+    }
+    if (!wait && p->rtc_job.wait_for(std::chrono::seconds(0)) != std::future_status::ready)
+        return PCG_OK; // still compiling: the interpreter kernel runs meanwhile
+    auto [code, err] = p->rtc_job.get();
+    if (code.empty()) {
+        p->rtc_state = -1;
+        p->rtc_err = "plan specialisation: " + err;
+        return fail(PCG_E_HIP, p->rtc_err);
+    }
+    if (p->device < 0) { // host-only plan: the source compiles; nothing to load
+        p->rtc_state = 0;
+        p->kernel = "scq_rtc_kernel";
+        return PCG_OK;
+    }
+    hipError_t e = hipModuleLoadData(&p->rtc_mod, code.data());
+    if (e == hipSuccess)
+        e = hipModuleGetFunction(&p->rtc_fn, p->rtc_mod, "scq_rtc_kernel");
+    if (e != hipSuccess) {
+        if (p->rtc_mod)
+            (void)hipModuleUnload(p->rtc_mod);
+        p->rtc_mod = nullptr;
+        p->rtc_fn = nullptr;
+        p->rtc_state = -1;
+        p->rtc_err = std::string("plan specialisation: module load: ") + hipGetErrorString(e);
+        return fail(PCG_E_HIP, p->rtc_err);
+    }
+    p->rtc_state = 1;
+    p->kernel = "scq_rtc_kernel";
+    return PCG_OK;
 }
 
 // lanes per codeword of an adaptive plan's SCL stage, 0 = list_pow2(L).  Measured on
@@ -358,6 +435,8 @@ static int plan_create_impl(pcg_plan** out,
         }
     }
     p->kernel = kernel_name(p->host, p->scl_lp);
+    if (const char* e = getenv("PCG_RTC")) // 0: interpreter only, 1: specialise at the first decode
+        p->rtc_mode = e[0] == '0' ? 0 : (e[0] == '1' ? 1 : 2);
     p->dev_opprof = getenv("PCG_OPPROF") != nullptr;
     if (p->dev_opprof)
         p->dev_overrides |= PCG_DEV_OPPROF;
@@ -565,7 +644,25 @@ int pcg_plan_describe(const pcg_plan* p, pcg_plan_desc* d)
                           : (p->host.L == 1 && p->host.sc_kind == 2 ? p->host.scq_q : 0);
     d->dev_overrides = p->dev_overrides | (p->fast ? p->fast->dev_overrides : 0u);
     d->recomputed_stages = p->host.L > 1 && !p->host.fixed ? p->scl_virt : 0u;
+    d->specialized = p->rtc_state == 1 ? 1u : 0u;
     return PCG_OK;
+}
+
+int pcg_plan_specialize(pcg_plan* p)
+{
+    if (!p)
+        return fail(PCG_E_ARG, "null plan");
+    if (p->fast) // adaptive plans: their Fast-SSC stage
+        p = p->fast;
+    if (!rtc_capable(p))
+        return fail(PCG_E_UNSUPPORTED, "no plan-specialised kernel for this plan (Fast-SSC float plans on the "
+                                       "LDS-resident kernel only; not with PCG_OPPROF)");
+    if (p->device < 0)
+        return specialize(p);
+    DeviceGuard g(p->device);
+    if (!g.ok)
+        return fail(PCG_E_HIP, "hipSetDevice failed");
+    return specialize(p);
 }
 
 static int decode_impl(pcg_plan* p,
@@ -711,7 +808,11 @@ static int decode_impl(pcg_plan* p,
         a.units = (uint32_t)pcg::wave_units(F, 64 / h.scq_q, p->wave_cap);
         a.ops = p->d_ops + h.ops.size(); // the fused schedule (plan.cpp fuse_sc16)
         a.nops = (uint32_t)h.ops_fused.size();
-        rc = pcg::launch_scq(a, h.scq_q, h.scq_virt != 0, s);
+        if ((p->rtc_state == 0 && rtc_capable(p) &&
+             (p->rtc_mode == 1 || (p->rtc_mode == 2 && F >= RTC_AUTO_FRAMES))) ||
+            p->rtc_state == 2)
+            (void)specialize(p, p->rtc_mode == 1); // on failure the interpreter runs (rtc_err says why)
+        rc = p->rtc_state == 1 ? pcg::scq_rtc_launch(p->rtc_fn, a, s) : pcg::launch_scq(a, h.scq_q, h.scq_virt != 0, s);
     } else if (h.L == 1 && h.sc_kind == 0) {
         a.units = (uint32_t)pcg::wave_units(F, 64, p->wave_cap);
         if ((rc = grow_scratch(p, a.units, sizeof(float), s)) != 0)

@@ -1,8 +1,10 @@
 // kernels.hpp -- device launch interface shared by the C ABI and the kernels.
 #pragma once
+#ifndef PCG_RTC
 #include <hip/hip_runtime.h>
-#include <stdint.h>
 #include <stdlib.h>
+#endif
+#include <stdint.h>
 
 namespace pcg {
 
@@ -59,6 +61,7 @@ struct KernelArgs {
     uint32_t scl_sb;
 };
 
+#ifndef PCG_RTC
 // PCG_*_WPC developer overrides of the waves per CU: ignored unless a positive number
 inline uint64_t env_wpc(const char* name, uint64_t dflt)
 {
@@ -69,6 +72,7 @@ inline uint64_t env_wpc(const char* name, uint64_t dflt)
     }
     return dflt;
 }
+#endif
 
 // Dynamic group assignment for the persistent lane-serial kernels (KernelArgs::queue;
 // one-wave workgroups). Every lane gets the same ticket; a wave stops at its first ticket
@@ -82,6 +86,7 @@ __device__ inline uint64_t queue_next(uint32_t* q)
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
 }
 
+#ifndef PCG_RTC
 // LDS floats one SC codeword needs: alpha (N floats, index 0 unused) + packed bits.
 inline uint32_t sc_wave_lds_floats(uint32_t N) { return N + (N >= 64 ? N / 32 : 2) + 2; }
 
@@ -89,9 +94,11 @@ int launch_sc(const KernelArgs& a, hipStream_t stream); // one codeword per wave
 uint32_t sc_soft_lds_bytes(uint32_t N);                  // 0: N too large for the soft-output decode
 int launch_sc_char(const KernelArgs& a, hipStream_t stream);   // FastSscFipChar (sc_char_kernel.hip)
 int launch_scl_char(const KernelArgs& a, hipStream_t stream);  // SclFipChar (scl_char_kernel.hip)
+#endif // PCG_RTC
 
 } // namespace pcg
 
+#ifndef PCG_RTC
 namespace pcg {
 // Persistent lane-serial kernels: per-wave LDS / global scratch layout, the wave cap of a
 // launch on the current device (CUs x resident waves per CU from hipOccupancy; evaluated
@@ -123,3 +130,4 @@ int sccs_layout(uint32_t N, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratc
 uint64_t sccs_wave_cap(uint32_t lds_dwords, bool i8);
 int launch_sccs(const KernelArgs& a, hipStream_t stream);
 } // namespace pcg
+#endif // PCG_RTC

@@ -6,8 +6,10 @@
 // frozen-set split        : splitFrozenBits,           src/polarcode/polarcode.cpp:14-34
 #pragma once
 #include <cstdint>
+#ifndef PCG_RTC // (plan-specialised kernels compile the device part of this header with hiprtc)
 #include <string>
 #include <vector>
+#endif
 
 #if defined(__HIPCC__) || defined(__HIP__)
 #define PCG_HD __host__ __device__
@@ -86,12 +88,13 @@ enum OpCode : uint32_t {
 // size-2 children when it is a RateR (ST_R0, ST_R1, ST_REP).
 enum StKind : uint32_t { ST_R0 = 0, ST_R1 = 1, ST_REP = 2, ST_SPC = 3, ST_RATER = 4 };
 
-PCG_HD inline uint32_t op_code(uint32_t w) { return w & 0xffu; }
-PCG_HD inline uint32_t op_stage(uint32_t w) { return (w >> 8) & 0xffu; }
-PCG_HD inline uint32_t op_off(uint32_t w) { return w >> 16; }
+constexpr PCG_HD inline uint32_t op_code(uint32_t w) { return w & 0xffu; }
+constexpr PCG_HD inline uint32_t op_stage(uint32_t w) { return (w >> 8) & 0xffu; }
+constexpr PCG_HD inline uint32_t op_off(uint32_t w) { return w >> 16; }
 // ops of the fused schedule followed by a descriptor word
-PCG_HD inline bool op_has_desc(uint32_t code) { return code >= 28 && code <= 31; }
+constexpr PCG_HD inline bool op_has_desc(uint32_t code) { return code >= 28 && code <= 31; }
 
+#ifndef PCG_RTC
 struct PlanHost {
     uint32_t N = 0, K = 0, L = 1, log2N = 0;
     int systematic = 1;
@@ -122,5 +125,6 @@ int build_plan(PlanHost& p,
                int crc_kind,
                std::string* err,
                int fixed = 0);
+#endif
 
 } // namespace pcg

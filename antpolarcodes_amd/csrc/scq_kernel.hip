@@ -20,8 +20,10 @@
 #include "plan.hpp"
 #include "wave.hpp"
 
+#ifndef PCG_RTC
 #include <stdio.h>
 #include <stdlib.h>
+#endif
 
 namespace pcg {
 
@@ -31,9 +33,9 @@ constexpr float FLT_MAX_Q = 3.40282347e+38f;
 
 // per-codeword LDS region: alpha floats (stage s at 2^s; stages < log2 N, or < log2 N - 1
 // when the root's children are recomputed from the channel, V), bit words, pad
-__host__ __device__ inline uint32_t scq_words(uint32_t N) { return N >= 32 ? N / 32 : 1u; }
-__host__ __device__ inline uint32_t scq_alpha(uint32_t N, bool V) { return V ? N / 2 : N; }
-__host__ __device__ inline uint32_t scq_region(uint32_t N, bool V)
+constexpr __host__ __device__ inline uint32_t scq_words(uint32_t N) { return N >= 32 ? N / 32 : 1u; }
+constexpr __host__ __device__ inline uint32_t scq_alpha(uint32_t N, bool V) { return V ? N / 2 : N; }
+constexpr __host__ __device__ inline uint32_t scq_region(uint32_t N, bool V)
 {
     // + 4 dwords so that codeword regions of one wave start on different LDS banks
     return ((scq_alpha(N, V) + scq_words(N) + 3u) & ~3u) + 4u;
@@ -1139,6 +1141,81 @@ PCG_DEV void bits_q(const Cw<Q>& w, uint32_t code, uint32_t s, uint32_t o)
     }
 }
 
+// One schedule op (plus the parent COMBs folded into it), then a wave barrier
+template <int Q>
+PCG_DEV void scq_op(Cw<Q>& w, uint32_t op, uint32_t desc)
+{
+    const uint32_t code = op_code(op), s = op_stage(op) & 15u, o = op_off(op);
+    const uint32_t up = op_stage(op) >> 4; // parent COMB levels folded into this op
+    if (op_has_desc(code)) {
+        if constexpr (Q >= 16)
+            q16_par<Q>(w, code, o, desc);
+        else if (code == OP_Q16F || code == OP_Q16G)
+            q16x<Q>(w, code, o, desc);
+        else
+            q16<Q>(w, code, o, desc);
+    } else if (code >= OP_L_R0)
+        leaf_q<Q>(w, code, s, o);
+    else if (code == OP_COMB || code == OP_COPY0)
+        bits_q<Q>(w, code, s, o);
+    else
+        inner_q<Q>(w, code, s, o);
+    // the folded parent COMBs, up the right spine: child (sc, oc) -> parent (sc+1, oc - 2^sc)
+    for (uint32_t l = 0, sc = s, oc = o; l < up; ++l, oc -= 1u << sc, ++sc) {
+        wsync();
+        bits_q<Q>(w, OP_COMB, sc + 1, oc - (1u << sc));
+    }
+    wsync();
+}
+
+// After the walk: non-systematic re-encode, detector syndrome, info bytes and the ok flag
+// of this lane's codeword.  N, W, K, kb, crc_bits and systematic are plan constants (literal
+// in a plan-specialised kernel).
+template <int Q>
+PCG_DEV void scq_output(const Cw<Q>& w, const KernelArgs& a, uint64_t frame, bool fok, uint32_t N, uint32_t W,
+                        uint32_t K, uint32_t kb, uint32_t crc_bits, int systematic)
+{
+    // non-systematic: re-encode x -> u in place (ButterflyFipPacked transform)
+    if (!systematic) {
+        for (uint32_t q = w.sub; q < W; q += Q)
+            w.row[q] = transform_word(w.row[q], N);
+        wsync();
+        for (uint32_t d = 1; d < W; d <<= 1) {
+            for (uint32_t q = w.sub; q < W; q += Q)
+                if (!(q & d))
+                    w.row[q] ^= w.row[q + d];
+            wsync();
+        }
+    }
+    // detector syndrome (affine GF(2) model, plan.cpp): bit r = c0_r ^ parity(cw & row_r)
+    uint32_t syn = 0;
+    for (uint32_t q = w.sub; q < W; q += Q) {
+        const uint32_t cwq = w.row[q];
+#pragma unroll 8
+        for (uint32_t rb = 0; rb < crc_bits; ++rb)
+            syn ^= (__builtin_popcount(cwq & a.crc_rows[rb * W + q]) & 1u) << rb;
+    }
+    syn = grp_xor(syn, Q) ^ a.crc_c0;
+    if (fok) {
+        // info bytes: the 8 positions of byte b are one 16-byte load (info_pos is padded)
+        uint8_t* out = a.info + frame * kb;
+        for (uint32_t b = w.sub; b < kb; b += Q) {
+            const uint4 pp = *reinterpret_cast<const uint4*>(a.info_pos + 8 * b);
+            const uint32_t pos[8] = { pp.x & 0xffffu, pp.x >> 16, pp.y & 0xffffu, pp.y >> 16,
+                                      pp.z & 0xffffu, pp.z >> 16, pp.w & 0xffffu, pp.w >> 16 };
+            uint32_t byte = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < 8; ++q)
+                if (8 * b + q < K)
+                    byte |= ((w.row[pos[q] >> 5] >> (pos[q] & 31u)) & 1u) << (7 - q);
+            out[b] = (uint8_t)byte;
+        }
+        if (a.ok && w.sub == 0)
+            a.ok[frame] = syn == 0 ? 1 : 0;
+    }
+    wsync();
+}
+
 // PROF (development aid, PCG_OPPROF=1): s_memtime cycles and counts per op code in
 // a.prof[2 * code], a.prof[2 * code + 1], kept in LDS and flushed once per wave
 template <int Q, bool V, bool PROF>
@@ -1172,33 +1249,17 @@ __global__ void __launch_bounds__(64, 4) scq_kernel(KernelArgs a)
         for (uint32_t k = 0; k < a.nops; ++k) {
             const uint32_t op = nxt; // the next schedule word is loaded while this op runs
             nxt = ld_const(a.ops, k + 1 < a.nops ? k + 1 : k);
-            const uint32_t code = op_code(op), s = op_stage(op) & 15u, o = op_off(op);
-            const uint32_t up = op_stage(op) >> 4; // parent COMB levels folded into this op
-            if (op_has_desc(code)) {
-                const uint32_t desc = nxt; // the descriptor word follows
+            uint32_t desc = 0;
+            if (op_has_desc(op_code(op))) {
+                desc = nxt; // the descriptor word follows
                 ++k;
                 nxt = ld_const(a.ops, k + 1 < a.nops ? k + 1 : k);
-                if constexpr (Q >= 16)
-                    q16_par<Q>(w, code, o, desc);
-                else if (code == OP_Q16F || code == OP_Q16G)
-                    q16x<Q>(w, code, o, desc);
-                else
-                    q16<Q>(w, code, o, desc);
-            } else if (code >= OP_L_R0)
-                leaf_q<Q>(w, code, s, o);
-            else if (code == OP_COMB || code == OP_COPY0)
-                bits_q<Q>(w, code, s, o);
-            else
-                inner_q<Q>(w, code, s, o);
-            // the folded parent COMBs, up the right spine: child (sc, oc) -> parent (sc+1, oc - 2^sc)
-            for (uint32_t l = 0, sc = s, oc = o; l < up; ++l, oc -= 1u << sc, ++sc) {
-                wsync();
-                bits_q<Q>(w, OP_COMB, sc + 1, oc - (1u << sc));
             }
-            wsync();
+            scq_op<Q>(w, op, desc);
             if constexpr (PROF) {
                 const uint64_t t1 = __builtin_amdgcn_s_memtime();
                 if (lane == 0) {
+                    const uint32_t code = op_code(op), s = op_stage(op) & 15u;
                     const uint32_t slot = (code & 31u) + (s >= 8 ? 32u : 0u); // large nodes apart
                     lprof[2 * slot] += t1 - t0;
                     lprof[2 * slot + 1] += 1;
@@ -1206,45 +1267,7 @@ __global__ void __launch_bounds__(64, 4) scq_kernel(KernelArgs a)
                 t0 = t1;
             }
         }
-        // non-systematic: re-encode x -> u in place (ButterflyFipPacked transform)
-        if (!a.systematic) {
-            for (uint32_t q = w.sub; q < W; q += Q)
-                w.row[q] = transform_word(w.row[q], a.N);
-            wsync();
-            for (uint32_t d = 1; d < W; d <<= 1) {
-                for (uint32_t q = w.sub; q < W; q += Q)
-                    if (!(q & d))
-                        w.row[q] ^= w.row[q + d];
-                wsync();
-            }
-        }
-        // detector syndrome (affine GF(2) model, plan.cpp): bit r = c0_r ^ parity(cw & row_r)
-        uint32_t syn = 0;
-        for (uint32_t q = w.sub; q < W; q += Q) {
-            const uint32_t cwq = w.row[q];
-#pragma unroll 8
-            for (uint32_t rb = 0; rb < a.crc_bits; ++rb)
-                syn ^= (__builtin_popcount(cwq & a.crc_rows[rb * W + q]) & 1u) << rb;
-        }
-        syn = grp_xor(syn, Q) ^ a.crc_c0;
-        if (fok) {
-            // info bytes: the 8 positions of byte b are one 16-byte load (info_pos is padded)
-            uint8_t* out = a.info + frame * a.kb;
-            for (uint32_t b = w.sub; b < a.kb; b += Q) {
-                const uint4 pp = *reinterpret_cast<const uint4*>(a.info_pos + 8 * b);
-                const uint32_t pos[8] = { pp.x & 0xffffu, pp.x >> 16, pp.y & 0xffffu, pp.y >> 16,
-                                          pp.z & 0xffffu, pp.z >> 16, pp.w & 0xffffu, pp.w >> 16 };
-                uint32_t byte = 0;
-#pragma unroll
-                for (uint32_t q = 0; q < 8; ++q)
-                    if (8 * b + q < a.K)
-                        byte |= ((w.row[pos[q] >> 5] >> (pos[q] & 31u)) & 1u) << (7 - q);
-                out[b] = (uint8_t)byte;
-            }
-            if (a.ok && w.sub == 0)
-                a.ok[frame] = syn == 0 ? 1 : 0;
-        }
-        wsync();
+        scq_output<Q>(w, a, frame, fok, a.N, W, a.K, a.kb, a.crc_bits, a.systematic);
         if constexpr (PROF) {
             const uint64_t t1 = __builtin_amdgcn_s_memtime();
             if (lane == 0) {
@@ -1260,6 +1283,57 @@ __global__ void __launch_bounds__(64, 4) scq_kernel(KernelArgs a)
                 atomicAdd(&a.prof[b], lprof[b]);
     }
 }
+
+#ifdef PCG_RTC
+// Plan-specialised Fast-SSC kernel (jit.cpp): the source that hiprtc compiles defines the
+// plan's fused schedule as PCG_RTC_OPS and its constants (PCG_RTC_Q, _V, _N, _LOG2N, _K,
+// _CRC, _SYS).  The walk is unrolled at compile time: every op's code, stage, offset and
+// descriptor are literals, so the dispatch branches, the schedule loads and the per-op
+// address arithmetic fold away and the compiler schedules across op boundaries.
+constexpr uint32_t rtc_ops[] = { PCG_RTC_OPS };
+constexpr uint32_t rtc_nops = sizeof(rtc_ops) / sizeof(rtc_ops[0]);
+
+template <int Q, uint32_t K>
+PCG_DEV void scq_walk(Cw<Q>& w)
+{
+    if constexpr (K < rtc_nops) {
+        constexpr uint32_t op = rtc_ops[K];
+        constexpr bool d = op_has_desc(op_code(op));
+        constexpr uint32_t desc = d ? rtc_ops[K + 1] : 0u;
+        scq_op<Q>(w, op, desc);
+        scq_walk<Q, K + (d ? 2u : 1u)>(w);
+    }
+}
+
+} // namespace
+
+extern "C" __global__ void __launch_bounds__(64, 4) scq_rtc_kernel(KernelArgs a)
+{
+    constexpr int Q = PCG_RTC_Q;
+    constexpr bool V = PCG_RTC_V != 0;
+    constexpr uint32_t N = PCG_RTC_N, G = 64 / Q;
+    constexpr uint32_t region = scq_region(N, V), W = scq_words(N);
+    extern __shared__ float smem_q[];
+    const uint32_t lane = threadIdx.x & 63, g = lane / Q;
+    Cw<Q> w;
+    w.alpha = smem_q + g * region;
+    w.row = reinterpret_cast<uint32_t*>(w.alpha + scq_alpha(N, V));
+    w.sub = lane & (Q - 1);
+    w.virt = V ? 1u : 0u;
+    w.root = 1u;
+    w.N = N;
+    w.top = PCG_RTC_LOG2N;
+    const uint64_t ngroups = (a.F + G - 1) / G;
+    for (uint64_t grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+        const uint64_t frame = grp * G + g;
+        const bool fok = frame < a.F;
+        w.y = a.llr + (fok ? frame : a.F - 1) * N;
+        scq_walk<Q, 0>(w);
+        scq_output<Q>(w, a, frame, fok, N, W, PCG_RTC_K, (PCG_RTC_K + 7) / 8, PCG_RTC_CRC, PCG_RTC_SYS);
+    }
+}
+
+#else // host side: layouts, occupancy, launch
 
 template <int Q, bool V>
 int scq_resident(uint32_t lds_bytes)
@@ -1333,5 +1407,7 @@ int launch_scq(const KernelArgs& a, uint32_t Q, bool V, hipStream_t stream)
 #undef PCG_SCQ_LAUNCH
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
+
+#endif // PCG_RTC
 
 } // namespace pcg

@@ -1,6 +1,8 @@
 // wave.hpp -- wave64 helpers shared by the CDNA4 decoder kernels.
 #pragma once
+#ifndef PCG_RTC
 #include <hip/hip_runtime.h>
+#endif
 #include <stdint.h>
 
 namespace pcg {

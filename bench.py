@@ -152,6 +152,20 @@ def _counter_rows(outdir):
     return rows
 
 
+def specialize(plan):
+    """Plan-specialised kernel (pcg_plan_specialize: hiprtc, Fast-SSC float plans and the
+    adaptive plans' Fast-SSC stage) before the warmup, so its compile is never timed and the
+    kernel name is the one that runs.  PCG_RTC=0 keeps the interpreter kernel."""
+    from antpolarcodes_amd._native import PCG_E_UNSUPPORTED, PcgError
+    if os.environ.get("PCG_RTC") == "0":
+        return
+    try:
+        plan.specialize()
+    except PcgError as e:
+        if e.code != PCG_E_UNSUPPORTED:
+            raise
+
+
 def measure_traffic(args, kernel, frames):
     """FETCH_SIZE and WRITE_SIZE (one rocprofv3 --pmc pass each, as the guide requires)
     of the decode kernel over child runs of this script; per-launch median."""
@@ -380,6 +394,7 @@ def main(argv=None):
             probe = Plan(N, L, frozen, systematic=True, crc=crc, device=-1, adaptive=adaptive, fixed=fixed)
             # adaptive plans: the list stage's kernel (the dominant one, r02af stats: 61 % of the
             # step) -- its FETCH/WRITE per launch, over the CRC failures it decodes
+            specialize(probe)
             traffic, traffic_note = measure_traffic(args, probe.kernel_name(), F)
             probe.close()
         torch.cuda.set_device(local)
@@ -403,6 +418,7 @@ def main(argv=None):
             d_llr = torch.from_numpy(host_llr).to(dev)
             d_ref = torch.from_numpy(info_h).to(dev)
         plan = Plan(N, L, frozen, systematic=True, crc=crc, device=local, adaptive=adaptive, fixed=fixed)
+        specialize(plan)
         kernel = plan.kernel_name()
         kb = plan.kb
         d_info = torch.empty((F, kb), dtype=torch.uint8, device=dev)

@@ -106,6 +106,7 @@ typedef struct pcg_plan_desc {
     uint32_t recomputed_stages;  /* lane-serial SCL: top LLR stages recomputed from the channel
                                     where read instead of stored (1: the root's children, 2:
                                     also its grandchildren); 0 for the other kernels */
+    uint32_t specialized;        /* 1: decodes run the plan-specialised kernel (pcg_plan_specialize) */
 } pcg_plan_desc;
 
 #define PCG_DEV_SCL_LP 0x1   /* PCG_SCL_LP / PCG_ADAPT_LP (only when the caller passed 0) */
@@ -242,6 +243,17 @@ int pcg_plan_describe(const pcg_plan* plan, pcg_plan_desc* desc);
 /* Name of the kernel a decode on this plan launches (e.g. "sclls_kernel<8>",
  * "scs_kernel"), as it appears in rocprofv3 kernel traces; "" for NULL. */
 const char* pcg_plan_kernel_name(const pcg_plan* plan);
+
+/* Compile (hiprtc, at run time, cached per process and code) and load a kernel specialised
+ * to this plan's code: the LDS-resident Fast-SSC kernel with the plan's decoder tree as a
+ * compile-time schedule -- the same device code and arithmetic as the interpreter kernel, so
+ * the same outputs bit for bit.  This replaces the reference's per-code decoder object tree
+ * (FastSscAvx::createDecoder, fastssc_avx_float.cpp:797-896) with per-code machine code.
+ * Fast-SSC float plans do this by themselves at their first decode of >= 8192 frames
+ * (PCG_RTC=0 never, PCG_RTC=1 at the first decode of any size).  Takes seconds the first time
+ * for a code.  PCG_E_UNSUPPORTED for other plans; on a host-only plan it only compiles.  On
+ * failure (e.g. no hiprtc) the plan keeps decoding with the interpreter kernel. */
+int pcg_plan_specialize(pcg_plan* plan);
 
 /* SCL plans: the metric path 0 starts every frame of later decode calls with.  0 (the
  * default) is a freshly constructed reference decoder; passing the previous frame's final

@@ -1,0 +1,88 @@
+"""GPU parity of the plan-specialised Fast-SSC kernel (rtc.cpp, pcg_plan_specialize) against
+the oracle, bit-exact: the same device code as the interpreter kernel compiled with the plan's
+schedule as literals, so every leaf kind, stage size, detector and the non-systematic
+re-encode must give the interpreter's (= the oracle's) bits."""
+import numpy as np
+import pytest
+
+from helpers import LLR_KINDS, llr_kinds, node_cover_sets
+
+pytestmark = pytest.mark.gpu
+
+
+def _spec_plan(N, frozen, systematic=True, crc=8):
+    from antpolarcodes_amd._native import Plan
+    p = Plan(N, 1, frozen, systematic=systematic, crc=crc, device=0)
+    p.specialize()
+    assert p.describe()["specialized"] == 1
+    assert p.kernel_name() == "scq_rtc_kernel"
+    return p
+
+
+def _check(oracle, p, N, frozen, llr, systematic=True, crc=8):
+    gi, gok, _ = p.decode_host(llr)
+    oi, ook = oracle.sc_decode(N, frozen, llr, systematic=systematic, crc=crc)
+    bad = np.nonzero(~(gi == oi).all(axis=1))[0]
+    assert bad.size == 0, f"N={N} K={N - len(frozen)} info mismatch in frames {bad[:8]}"
+    assert np.array_equal(gok, ook)
+
+
+@pytest.mark.parametrize("N", [8, 32, 128, 512, 1024, 2048, 4096])
+def test_rtc_bb_codes(oracle, N):
+    rng = np.random.default_rng(100 + N)
+    K = max(8, N // 2)
+    fr = oracle.frozen_bits_bb(N, K, 0.0)
+    p = _spec_plan(N, fr)
+    for kind in LLR_KINDS:
+        _check(oracle, p, N, fr, llr_kinds(rng, 96, N, kind))
+
+
+@pytest.mark.parametrize("systematic", [True, False])
+@pytest.mark.parametrize("crc", [0, 16, 32])
+def test_rtc_crc_and_systematic(oracle, systematic, crc):
+    rng = np.random.default_rng(5)
+    fr = oracle.frozen_bits_bb(1024, 512, 0.0)
+    p = _spec_plan(1024, fr, systematic, crc)
+    _check(oracle, p, 1024, fr, llr_kinds(rng, 256, 1024, "normal"), systematic, crc)
+
+
+def test_rtc_node_kinds(oracle):
+    """Every Fast-SSC leaf kind (incl. the ZeroSpc quirk Q1) through specialised kernels."""
+    rng = np.random.default_rng(13)
+    done = 0
+    for N, fr in node_cover_sets():
+        try:
+            oracle.sc_tree(N, fr)
+        except ValueError:
+            continue
+        p = _spec_plan(N, fr)
+        for kind in ("normal", "ints", "zeros"):
+            _check(oracle, p, N, fr, llr_kinds(rng, 64, N, kind))
+        done += 1
+    assert done > 0
+
+
+def test_rtc_auto_large_batch_config2(oracle):
+    """Config 2 (N=1024, K=512, CRC-8): a batch of >= 8192 frames starts the plan's
+    specialisation in the background (the interpreter kernel decodes meanwhile); once it is
+    loaded the same batch decodes through it.  Both match the oracle."""
+    import torch
+    from antpolarcodes_amd import frames
+    from antpolarcodes_amd._native import Plan
+    N, K = 1024, 512
+    fr = oracle.frozen_bits_bb(N, K, 0.0)
+    llr, _, _ = frames.awgn_frames(N, fr, 8192, 2.0, seed=21, crc=8)
+    p = Plan(N, 1, fr, crc=8, device=0)
+    assert p.describe()["specialized"] == 0
+    x = torch.from_numpy(np.ascontiguousarray(llr, dtype=np.float32)).cuda()
+    oi, ook = oracle.sc_decode(N, fr, llr, crc=8)
+    for rnd in range(2):
+        info = torch.zeros((x.shape[0], p.kb), dtype=torch.uint8, device="cuda")
+        ok = torch.zeros(x.shape[0], dtype=torch.uint8, device="cuda")
+        p.decode_device(x, info, ok)
+        torch.cuda.synchronize()
+        assert np.array_equal(info.cpu().numpy(), oi), f"round {rnd}"
+        assert np.array_equal(ok.cpu().numpy(), ook), f"round {rnd}"
+        p.specialize()  # waits for the background compile
+        assert p.describe()["specialized"] == 1
+        assert p.kernel_name() == "scq_rtc_kernel"
