@@ -74,6 +74,8 @@ struct pcg_plan {
     // -1 = failed (rtc_err)
     int rtc_mode = 2;
     int rtc_state = 0;
+    bool walk_latency = false; // an adaptive plan's list stage
+    bool rtc_scl = false;      // PCG_RTC_SCL=1 (dev): list plans specialise too
     std::future<std::pair<std::vector<char>, std::string>> rtc_job;
     std::string rtc_err;
     hipModule_t rtc_mod = nullptr;
@@ -161,9 +163,24 @@ void free_plan_device(pcg_plan* p)
 // hiprtc compile takes seconds once per code and process; smaller batches are latency work).
 constexpr uint64_t RTC_AUTO_FRAMES = 8192;
 
+// Plans with a specialised kernel: Fast-SSC float plans on the LDS-resident kernel; never
+// with the developer op profiler.  Float list plans only behind the PCG_RTC_SCL=1 dev switch
+// (their layout and plan constants as literals, the schedule loop kept: a fully unrolled walk
+// -- 280 schedule words for config 3, each op inlining path selection and the leaf decoders
+// -- had not compiled after 20 minutes, against 34 s for config 2's 60 fused Fast-SSC ops).
 bool rtc_capable(const pcg_plan* p)
 {
-    return !p->host.fixed && p->host.L == 1 && p->host.sc_kind == 2 && !p->dev_opprof;
+    if (p->host.fixed || p->dev_opprof)
+        return false;
+    return p->host.L == 1 ? p->host.sc_kind == 2 : (p->rtc_scl && !p->walk_latency);
+}
+
+std::string rtc_source(const pcg_plan* p)
+{
+    if (p->host.L == 1)
+        return pcg::scq_rtc_source(p->host);
+    return pcg::scl_rtc_source(p->host, p->scl_lp, p->lds_stage_limit, p->scl_virt, p->scl_v3, p->scl_sb,
+                               p->scl_fuse);
 }
 
 // Compile (hiprtc, cached per process and on disk) and, on a device plan, load the plan's
@@ -177,10 +194,9 @@ int specialize(pcg_plan* p, bool wait = true)
     if (p->rtc_state == -1)
         return fail(PCG_E_HIP, p->rtc_err);
     if (p->rtc_state == 0) {
-        pcg::PlanHost host = p->host; // the job's own copy
-        p->rtc_job = std::async(std::launch::async, [host] {
+        p->rtc_job = std::async(std::launch::async, [src = rtc_source(p)] {
             std::pair<std::vector<char>, std::string> r;
-            if (pcg::scq_rtc_compile(host, &r.first, &r.second) != 0)
+            if (pcg::rtc_compile(src, &r.first, &r.second) != 0)
                 r.first.clear();
             return r;
         });
@@ -196,12 +212,12 @@ int specialize(pcg_plan* p, bool wait = true)
     }
     if (p->device < 0) { // host-only plan: the source compiles; nothing to load
         p->rtc_state = 0;
-        p->kernel = "scq_rtc_kernel";
+        p->kernel = p->host.L == 1 ? "scq_rtc_kernel" : "scl_rtc_kernel";
         return PCG_OK;
     }
     hipError_t e = hipModuleLoadData(&p->rtc_mod, code.data());
     if (e == hipSuccess)
-        e = hipModuleGetFunction(&p->rtc_fn, p->rtc_mod, "scq_rtc_kernel");
+        e = hipModuleGetFunction(&p->rtc_fn, p->rtc_mod, p->host.L == 1 ? "scq_rtc_kernel" : "scl_rtc_kernel");
     if (e != hipSuccess) {
         if (p->rtc_mod)
             (void)hipModuleUnload(p->rtc_mod);
@@ -212,7 +228,7 @@ int specialize(pcg_plan* p, bool wait = true)
         return fail(PCG_E_HIP, p->rtc_err);
     }
     p->rtc_state = 1;
-    p->kernel = "scq_rtc_kernel";
+    p->kernel = p->host.L == 1 ? "scq_rtc_kernel" : "scl_rtc_kernel";
     return PCG_OK;
 }
 
@@ -435,6 +451,11 @@ static int plan_create_impl(pcg_plan** out,
         }
     }
     p->kernel = kernel_name(p->host, p->scl_lp);
+    p->walk_latency = walk_latency;
+    if (const char* e = getenv("PCG_RTC_SCL"); e && e[0] == '1') {
+        p->rtc_scl = true;
+        p->dev_overrides |= PCG_DEV_LAYOUT;
+    }
     if (const char* e = getenv("PCG_RTC")) // 0: interpreter only, 1: specialise at the first decode
         p->rtc_mode = e[0] == '0' ? 0 : (e[0] == '1' ? 1 : 2);
     p->dev_opprof = getenv("PCG_OPPROF") != nullptr;
@@ -655,8 +676,8 @@ int pcg_plan_specialize(pcg_plan* p)
     if (p->fast) // adaptive plans: their Fast-SSC stage
         p = p->fast;
     if (!rtc_capable(p))
-        return fail(PCG_E_UNSUPPORTED, "no plan-specialised kernel for this plan (Fast-SSC float plans on the "
-                                       "LDS-resident kernel only; not with PCG_OPPROF)");
+        return fail(PCG_E_UNSUPPORTED, "no plan-specialised kernel for this plan (float Fast-SSC plans only; "
+                                       "not with PCG_OPPROF)");
     if (p->device < 0)
         return specialize(p);
     DeviceGuard g(p->device);
@@ -812,7 +833,7 @@ static int decode_impl(pcg_plan* p,
              (p->rtc_mode == 1 || (p->rtc_mode == 2 && F >= RTC_AUTO_FRAMES))) ||
             p->rtc_state == 2)
             (void)specialize(p, p->rtc_mode == 1); // on failure the interpreter runs (rtc_err says why)
-        rc = p->rtc_state == 1 ? pcg::scq_rtc_launch(p->rtc_fn, a, s) : pcg::launch_scq(a, h.scq_q, h.scq_virt != 0, s);
+        rc = p->rtc_state == 1 ? pcg::rtc_launch(p->rtc_fn, a, s) : pcg::launch_scq(a, h.scq_q, h.scq_virt != 0, s);
     } else if (h.L == 1 && h.sc_kind == 0) {
         a.units = (uint32_t)pcg::wave_units(F, 64, p->wave_cap);
         if ((rc = grow_scratch(p, a.units, sizeof(float), s)) != 0)
@@ -833,7 +854,11 @@ static int decode_impl(pcg_plan* p,
             if (e != hipSuccess)
                 return hip_fail(e, "hipMemsetAsync(work queue)");
         }
-        rc = pcg::launch_sclls(a, s);
+        if ((p->rtc_state == 0 && rtc_capable(p) &&
+             (p->rtc_mode == 1 || (p->rtc_mode == 2 && F >= RTC_AUTO_FRAMES))) ||
+            p->rtc_state == 2)
+            (void)specialize(p, p->rtc_mode == 1);
+        rc = p->rtc_state == 1 ? pcg::rtc_launch(p->rtc_fn, a, s) : pcg::launch_sclls(a, s);
     }
     if (rc != 0)
         return fail(rc, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));

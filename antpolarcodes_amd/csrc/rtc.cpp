@@ -1,12 +1,15 @@
-// rtc.cpp -- plan-specialised Fast-SSC kernels, compiled at run time with hiprtc.
+// rtc.cpp -- plan-specialised decoder kernels, compiled at run time with hiprtc.
 //
 // The reference builds one decoder object tree per code (FastSscAvx::createDecoder,
 // fastssc_avx_float.cpp:797-896) and walks it with virtual calls; scq_kernel.hip walks the
 // plan's flattened schedule as an interpreter (schedule words through the scalar cache, a
 // dispatch branch per op).  A plan-specialised kernel is the same device code compiled with
 // the plan's fused schedule as a compile-time array (scq_kernel.hip, PCG_RTC): every op is
-// inlined with literal codes, stages and offsets.  The source is scq_kernel.hip and the
-// headers it includes, embedded into the library at build time (build/rtc_src.inc).
+// inlined with literal codes, stages and offsets.  The same holds for the lane-serial list
+// decoder (sclls_kernel.hip; SclAvx::createDecoder, scl_avx_float.cpp:624-651), whose
+// layout constants and path counts become literals as well.  The sources are the kernel
+// files and the headers they include, embedded into the library at build time
+// (build/rtc_src.inc).
 //
 // hiprtc is opened with dlopen on first use, so a machine without it still loads libpcg and
 // decodes with the interpreter kernel.  Compiled code objects are cached per process by
@@ -118,7 +121,7 @@ std::string disk_path(const std::string& src)
         if (k == dir.size() || dir[k] == '/')
             (void)mkdir(dir.substr(0, k).c_str(), 0755);
     char name[32];
-    snprintf(name, sizeof(name), "/scq_%016llx.co", (unsigned long long)h);
+    snprintf(name, sizeof(name), "/pcg_%016llx.co", (unsigned long long)h);
     return dir + name;
 }
 
@@ -172,9 +175,32 @@ std::string scq_rtc_source(const PlanHost& h)
     return s;
 }
 
-int scq_rtc_compile(const PlanHost& h, std::vector<char>* code, std::string* err)
+std::string scl_rtc_source(const PlanHost& h, uint32_t lp, uint32_t Sl, uint32_t virt, uint32_t v3, uint32_t sb,
+                           uint32_t fuse)
 {
-    const std::string src = scq_rtc_source(h);
+    std::string s = "#define PCG_RTC 1\n";
+    auto def = [&](const char* k, uint32_t v) { s += std::string("#define PCG_RTC_") + k + " " + std::to_string(v) + "u\n"; };
+    def("LP", lp);
+    def("N", h.N);
+    def("LOG2N", h.log2N);
+    def("K", h.K);
+    def("L", h.L);
+    def("CRC", (uint32_t)h.crc_kind);
+    s += "#define PCG_RTC_SYS " + std::to_string(h.systematic ? 1 : 0) + "\n";
+    def("SL", Sl);
+    def("VIRT", virt);
+    def("V3", v3);
+    def("SB", sb);
+    def("FUSE", fuse);
+    s += "#define PCG_RTC_OPS";
+    for (size_t k = 0; k < h.ops.size(); ++k)
+        s += (k ? "," : " ") + std::to_string(h.ops[k]) + "u";
+    s += "\n#include \"sclls_kernel.hip\"\n";
+    return s;
+}
+
+int rtc_compile(const std::string& src, std::vector<char>* code, std::string* err)
+{
     if (const char* path = getenv("PCG_RTC_DUMP")) { // development aid: the generated source
         if (FILE* f = fopen(path, "w")) {
             fputs(src.c_str(), f);
@@ -201,7 +227,7 @@ int scq_rtc_compile(const PlanHost& h, std::vector<char>* code, std::string* err
         return -1;
     }
     hiprtcProgram prog = nullptr;
-    if (a.create(&prog, src.c_str(), "scq_rtc.hip", rtc_nsrcs, rtc_srcs, rtc_names) != HIPRTC_SUCCESS) {
+    if (a.create(&prog, src.c_str(), "pcg_rtc.hip", rtc_nsrcs, rtc_srcs, rtc_names) != HIPRTC_SUCCESS) {
         *err = "hiprtcCreateProgram failed";
         return -1;
     }
@@ -237,7 +263,7 @@ int scq_rtc_compile(const PlanHost& h, std::vector<char>* code, std::string* err
     return 0;
 }
 
-int scq_rtc_launch(hipFunction_t fn, const KernelArgs& a, hipStream_t stream)
+int rtc_launch(hipFunction_t fn, const KernelArgs& a, hipStream_t stream)
 {
     const uint64_t grid = a.units;
     if (grid == 0) // no waves for a non-empty batch: an error, never a silent no-op

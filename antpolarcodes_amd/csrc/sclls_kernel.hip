@@ -37,8 +37,10 @@
 #include "plan.hpp"
 #include "wave.hpp"
 
+#ifndef PCG_RTC
 #include <stdio.h>
 #include <stdlib.h>
+#endif
 
 namespace pcg {
 
@@ -71,16 +73,16 @@ struct LsLayout {
 // removes the largest per-path buffers and their HBM traffic.  Memory stages are
 // [3, mtop) with mtop = top-1 (or 3 when N = 8: no memory stage at all).
 // With virt = 2 stage top-2 is recomputed as well (from four channel LLRs).
-__host__ __device__ inline uint32_t ls_mtop(uint32_t top, uint32_t virt)
+constexpr __host__ __device__ inline uint32_t ls_mtop(uint32_t top, uint32_t virt)
 {
     const uint32_t m = top - virt;
     return m > 3u ? m : 3u;
 }
-__host__ __device__ inline uint32_t ls_max_virt(uint32_t top) { return top >= 9 ? 2u : (top >= 4 ? 1u : 0u); }
+constexpr __host__ __device__ inline uint32_t ls_max_virt(uint32_t top) { return top >= 9 ? 2u : (top >= 4 ? 1u : 0u); }
 
 // Global scratch slab of one wave: alpha stages [Sl, mtop), then the tie-fallback
 // candidate list (64 * 8 values + 64 * 8 ids; rarely touched, so not worth LDS).
-__host__ __device__ inline uint64_t ls_gl_alpha_floats(uint32_t mt, uint32_t Sl)
+constexpr __host__ __device__ inline uint64_t ls_gl_alpha_floats(uint32_t mt, uint32_t Sl)
 {
     return Sl < mt ? 64ull * ((1ull << mt) - (1ull << Sl)) : 0ull;
 }
@@ -90,26 +92,26 @@ __host__ __device__ inline uint64_t ls_gl_alpha_floats(uint32_t mt, uint32_t Sl)
 // LLRs from the parent's chunks (F for a left child, G with the left sibling's bits for a
 // right one: V3St, V4St), so the F / G ops writing them vanish and the LDS stages start at
 // 3 + vlow.
-__host__ __device__ inline uint32_t ls_abase(uint32_t vlow) { return 8u << vlow; } // alpha[s] at 64 * (2^s - base)
+constexpr __host__ __device__ inline uint32_t ls_abase(uint32_t vlow) { return 8u << vlow; } // alpha[s] at 64 * (2^s - base)
 
 // D buffers: D[s] at word ls_doff(s) of the lane's column (D[4], D[5]: one word each, D[s]
 // 2^(s-5) words at 2^(s-5); the N = 8 code's D[3] is D[4]'s word).  Stages [4, Sb) in
 // LDS, [Sb, top] in the global slab (Sb >= 5).
-__host__ __device__ inline uint32_t ls_doff(uint32_t s) { return s <= 4u ? 0u : 1u << (s - 5u); }
-__host__ __device__ inline uint32_t ls_dlds_words(uint32_t top, uint32_t Sb)
+constexpr __host__ __device__ inline uint32_t ls_doff(uint32_t s) { return s <= 4u ? 0u : 1u << (s - 5u); }
+constexpr __host__ __device__ inline uint32_t ls_dlds_words(uint32_t top, uint32_t Sb)
 {
     if (Sb == 0) // codeword rows: N bits per lane
         return top >= 5u ? 1u << (top - 5u) : 1u;
     const uint32_t e = Sb < top + 1u ? Sb : top + 1u;
     return e <= 5u ? 1u : 1u << (e - 5u);
 }
-__host__ __device__ inline uint32_t ls_dgl_words(uint32_t top, uint32_t Sb)
+constexpr __host__ __device__ inline uint32_t ls_dgl_words(uint32_t top, uint32_t Sb)
 {
     return Sb != 0 && Sb <= top ? (1u << (top - 4u)) - (1u << (Sb - 5u)) : 0u;
 }
-__host__ __device__ inline LsLayout ls_layout(uint32_t top, uint32_t Sl, uint32_t vlow, uint32_t Sb)
+constexpr __host__ __device__ inline LsLayout ls_layout(uint32_t top, uint32_t Sl, uint32_t vlow, uint32_t Sb)
 {
-    LsLayout y;
+    LsLayout y{};
     uint32_t o = 0;
     y.alpha = o;
     o += (1u << Sl) > ls_abase(vlow) ? 64u * ((1u << Sl) - ls_abase(vlow)) : 0u;
@@ -2078,8 +2080,70 @@ PCG_DEV uint32_t crc_syn(const DBits& cw, const uint32_t* rows, uint32_t W, uint
 #ifndef PCG_LS_MINW
 #define PCG_LS_MINW 2
 #endif
+// One op of the walk, then a wave barrier.  fuse: this F / G runs fused with the next
+// schedule op, the child's F (ls_fgf); desc: a size-8 subtree's descriptor word.
 template <int LP>
-__global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
+PCG_DEV void ls_op(Ls<LP>& c, uint32_t code, uint32_t s, uint32_t o, uint32_t& P, bool fuse, uint32_t desc)
+{
+    const bool act = c.p < P;
+    switch (code) {
+    case OP_F:
+        if (fuse)
+            ls_fgf_op<OP_F>(c, s, o, P);
+        else
+            ls_fg_op<OP_F>(c, s, o, P);
+        break;
+    case OP_G:
+        if (fuse)
+            ls_fgf_op<OP_G>(c, s, o, P);
+        else
+            ls_fg_op<OP_G>(c, s, o, P);
+        break;
+    case OP_COMB:
+        ls_comb(c, s, o, act);
+        break;
+    case OP_S_ST8:
+        with_stage(c, 3, o, [&](auto src) { ls_st8(c, src, desc, o, P); });
+        break;
+    case OP_S_R0:
+        with_stage(c, s, o, [&](auto src) { ls_r0(c, src, s, o, act); });
+        break;
+    default: // OP_S_R1 / OP_S_SPC (n >= 8)
+        with_stage(c, s, o, [&](auto src) { ls_branch_leaf(c, src, code, s, o, P); });
+        break;
+    }
+    wsync();
+}
+
+#ifdef PCG_RTC
+// Plan-specialised walk (rtc.cpp): the plan's schedule as literals (PCG_RTC_OPS), unrolled
+// at compile time with every op's code, stage, offset, fusion and descriptor constant
+// (PCG_RTC_UNROLL = 1; measured: config 3's kernel did not compile within 20 minutes).  By
+// default the specialised list kernel keeps the schedule loop and only its layout and plan
+// constants are literals (scl_rtc_kernel).
+constexpr uint32_t rtc_ops[] = { PCG_RTC_OPS };
+constexpr uint32_t rtc_nops = sizeof(rtc_ops) / sizeof(rtc_ops[0]);
+constexpr uint32_t rtc_mt = ls_mtop(PCG_RTC_LOG2N, PCG_RTC_VIRT);
+
+template <int LP, uint32_t K>
+PCG_DEV void ls_walk(Ls<LP>& c, uint32_t& P)
+{
+    if constexpr (K < rtc_nops) {
+        constexpr uint32_t w = rtc_ops[K];
+        constexpr uint32_t code = op_code(w), s = op_stage(w), o = op_off(w);
+        constexpr bool fuse = (code == OP_F || code == OP_G) && s >= 5 && s - 1 >= PCG_RTC_SL && s - 1 < rtc_mt &&
+                              (PCG_RTC_FUSE & 1u) && K + 1 < rtc_nops && op_code(rtc_ops[K + 1]) == OP_F &&
+                              op_stage(rtc_ops[K + 1]) == s - 1;
+        constexpr bool d = code == OP_S_ST8;
+        constexpr uint32_t desc = d ? rtc_ops[K + 1] : 0u;
+        ls_op<LP>(c, code, s, o, P, fuse, desc);
+        ls_walk<LP, K + (fuse || d ? 2u : 1u)>(c, P);
+    }
+}
+#endif
+
+template <int LP>
+PCG_DEV void sclls_body(const KernelArgs& a)
 {
     extern __shared__ float smem[];
     constexpr uint32_t G = 64 / LP;
@@ -2133,10 +2197,12 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
 #ifdef PCG_LS_PROF
         const uint64_t tf0 = __builtin_amdgcn_s_memtime();
 #endif
+#if defined(PCG_RTC) && PCG_RTC_UNROLL
+        ls_walk<LP, 0>(c, P);
+#else
         for (uint32_t kop = 0; kop < a.nops; ++kop) {
             const uint32_t w = ld_const(a.ops, kop);
             const uint32_t code = op_code(w), s = op_stage(w), o = op_off(w);
-            const bool act = c.p < P;
 #ifdef PCG_LS_PROF
             const uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -2148,37 +2214,10 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
                 const uint32_t w2 = ld_const(a.ops, kop + 1);
                 fuse = op_code(w2) == OP_F && op_stage(w2) == s - 1;
             }
-            switch (code) {
-            case OP_F:
-                if (fuse) {
-                    ls_fgf_op<OP_F>(c, s, o, P);
-                    ++kop;
-                } else
-                    ls_fg_op<OP_F>(c, s, o, P);
-                break;
-            case OP_G:
-                if (fuse) {
-                    ls_fgf_op<OP_G>(c, s, o, P);
-                    ++kop;
-                } else
-                    ls_fg_op<OP_G>(c, s, o, P);
-                break;
-            case OP_COMB:
-                ls_comb(c, s, o, act);
-                break;
-            case OP_S_ST8: {
-                const uint32_t desc = ld_const(a.ops, ++kop);
-                with_stage(c, 3, o, [&](auto src) { ls_st8(c, src, desc, o, P); });
-                break;
-            }
-            case OP_S_R0:
-                with_stage(c, s, o, [&](auto src) { ls_r0(c, src, s, o, act); });
-                break;
-            default: // OP_S_R1 / OP_S_SPC (n >= 8)
-                with_stage(c, s, o, [&](auto src) { ls_branch_leaf(c, src, code, s, o, P); });
-                break;
-            }
-            wsync();
+            const uint32_t desc = code == OP_S_ST8 ? ld_const(a.ops, kop + 1) : 0u;
+            ls_op<LP>(c, code, s, o, P, fuse, desc);
+            if (fuse || code == OP_S_ST8)
+                ++kop; // the fused child F / the subtree's descriptor word
 #ifdef PCG_LS_PROF
             {
                 const uint64_t t1 = __builtin_amdgcn_s_memtime();
@@ -2190,6 +2229,7 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
             }
 #endif
         }
+#endif
 #ifdef PCG_LS_PROF
         const uint64_t tf1 = __builtin_amdgcn_s_memtime();
 #endif
@@ -2273,7 +2313,38 @@ __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
 #endif
 }
 
+#ifndef PCG_RTC
+template <int LP>
+__global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
+{
+    sclls_body<LP>(a);
+}
+#endif
+
 } // namespace
+
+#ifdef PCG_RTC
+// the plan-specialised list decoder: the layout and the plan's constants are literals
+extern "C" __global__ void __launch_bounds__(64, PCG_LS_MINW) scl_rtc_kernel(KernelArgs a)
+{
+    KernelArgs b = a;
+    b.N = PCG_RTC_N;
+    b.log2N = PCG_RTC_LOG2N;
+    b.K = PCG_RTC_K;
+    b.kb = (PCG_RTC_K + 7u) / 8u;
+    b.L = PCG_RTC_L;
+    b.crc_bits = PCG_RTC_CRC;
+    b.systematic = PCG_RTC_SYS;
+    b.lds_stage_limit = PCG_RTC_SL;
+    b.scl_virt = PCG_RTC_VIRT;
+    b.scl_v3 = PCG_RTC_V3;
+    b.scl_sb = PCG_RTC_SB;
+    b.scl_fuse = PCG_RTC_FUSE;
+    b.scl_lp = PCG_RTC_LP;
+    b.nops = rtc_nops;
+    sclls_body<PCG_RTC_LP>(b);
+}
+#else // host side: layout, occupancy, launch
 
 #ifndef PCG_SCL_VIRT_DEFAULT
 #define PCG_SCL_VIRT_DEFAULT 3 // recomputed top stages (2: the quarters too, 3: eighths for LP >= 16, where sclls_layout allows)
@@ -2438,5 +2509,7 @@ int launch_sclls(const KernelArgs& a, hipStream_t stream)
 #endif
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
+
+#endif // PCG_RTC
 
 } // namespace pcg

@@ -26,7 +26,7 @@ def test_specialize_compiles_config2(oracle, tmp_path, monkeypatch):
     t = time.time()
     _host_plan(oracle, 1024, 512).specialize()  # same code: the process cache
     assert time.time() - t < max(0.5, first / 4)
-    files = list((tmp_path / "rtc").glob("scq_*.co"))  # and the disk cache, for other processes
+    files = list((tmp_path / "rtc").glob("pcg_*.co"))  # and the disk cache, for other processes
     assert len(files) == 1 and files[0].read_bytes()[:4] == b"\x7fELF"
 
 
