@@ -75,7 +75,7 @@ struct pcg_plan {
     int rtc_mode = 2;
     int rtc_state = 0;
     bool walk_latency = false; // an adaptive plan's list stage
-    bool rtc_scl = false;      // PCG_RTC_SCL=1 (dev): list plans specialise too
+    bool rtc_scl = true;       // list plans specialise too (PCG_RTC_SCL=0: not)
     std::future<std::pair<std::vector<char>, std::string>> rtc_job;
     std::string rtc_err;
     hipModule_t rtc_mod = nullptr;
@@ -163,11 +163,12 @@ void free_plan_device(pcg_plan* p)
 // hiprtc compile takes seconds once per code and process; smaller batches are latency work).
 constexpr uint64_t RTC_AUTO_FRAMES = 8192;
 
-// Plans with a specialised kernel: Fast-SSC float plans on the LDS-resident kernel; never
-// with the developer op profiler.  Float list plans only behind the PCG_RTC_SCL=1 dev switch
-// (their layout and plan constants as literals, the schedule loop kept: a fully unrolled walk
-// -- 280 schedule words for config 3, each op inlining path selection and the leaf decoders
-// -- had not compiled after 20 minutes, against 34 s for config 2's 60 fused Fast-SSC ops).
+// Plans with a specialised kernel: Fast-SSC float plans on the LDS-resident kernel (the walk
+// unrolled) and float list plans (their layout and plan constants as literals, the schedule
+// loop kept: a fully unrolled walk -- 280 schedule words for config 3, each op inlining path
+// selection and the leaf decoders -- had not compiled after 20 minutes, against 34 s for
+// config 2's 60 fused Fast-SSC ops; PCG_RTC_SCL=0 keeps list plans on the interpreter), not
+// an adaptive plan's list stage (a few frames per launch); never with the op profiler.
 bool rtc_capable(const pcg_plan* p)
 {
     if (p->host.fixed || p->dev_opprof)
@@ -452,8 +453,8 @@ static int plan_create_impl(pcg_plan** out,
     }
     p->kernel = kernel_name(p->host, p->scl_lp);
     p->walk_latency = walk_latency;
-    if (const char* e = getenv("PCG_RTC_SCL"); e && e[0] == '1') {
-        p->rtc_scl = true;
+    if (const char* e = getenv("PCG_RTC_SCL"); e && e[0] == '0') {
+        p->rtc_scl = false;
         p->dev_overrides |= PCG_DEV_LAYOUT;
     }
     if (const char* e = getenv("PCG_RTC")) // 0: interpreter only, 1: specialise at the first decode
@@ -676,8 +677,8 @@ int pcg_plan_specialize(pcg_plan* p)
     if (p->fast) // adaptive plans: their Fast-SSC stage
         p = p->fast;
     if (!rtc_capable(p))
-        return fail(PCG_E_UNSUPPORTED, "no plan-specialised kernel for this plan (float Fast-SSC plans only; "
-                                       "not with PCG_OPPROF)");
+        return fail(PCG_E_UNSUPPORTED, "no plan-specialised kernel for this plan (float Fast-SSC and list "
+                                       "plans; not the 8-bit decoders, not with PCG_OPPROF)");
     if (p->device < 0)
         return specialize(p);
     DeviceGuard g(p->device);

@@ -86,3 +86,23 @@ def test_rtc_auto_large_batch_config2(oracle):
         p.specialize()  # waits for the background compile
         assert p.describe()["specialized"] == 1
         assert p.kernel_name() == "scq_rtc_kernel"
+
+
+@pytest.mark.parametrize("N,K,L,crc,systematic", [(256, 128, 4, 16, True), (1024, 512, 8, 8, True),
+                                                  (512, 256, 6, 32, False)])
+def test_rtc_list_plans(oracle, N, K, L, crc, systematic):
+    """Specialised list plans (scl_rtc_kernel: the lane-serial kernel with the plan's layout and
+    constants as literals): info, ok and the ordered path metrics bit-exact."""
+    from antpolarcodes_amd._native import Plan
+    rng = np.random.default_rng(N + L)
+    fr = oracle.frozen_bits_bb(N, K, 0.0)
+    p = Plan(N, L, fr, systematic=systematic, crc=crc, device=0)
+    p.specialize()
+    assert p.describe()["specialized"] == 1 and p.kernel_name() == "scl_rtc_kernel"
+    for kind in LLR_KINDS:
+        llr = llr_kinds(rng, 64, N, kind)
+        gi, gok, gm = p.decode_host(llr, want_metrics=True)
+        oi, ook, om, _, _ = oracle.scl_decode(N, L, fr, llr, systematic=systematic, crc=crc, paths=True)
+        assert np.array_equal(gi, oi), kind
+        assert np.array_equal(gok, ook), kind
+        assert np.array_equal(gm.view(np.uint32), om.view(np.uint32)), kind

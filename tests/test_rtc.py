@@ -1,4 +1,4 @@
-"""Plan-specialised Fast-SSC kernels on the CPU: the generated hiprtc source compiles for
+"""Plan-specialised kernels on the CPU: the generated hiprtc source compiles for
 gfx950 (a host-only plan compiles without loading; no GPU needed) and the API refuses plans
 that have no specialised kernel."""
 import time
@@ -35,9 +35,17 @@ def test_specialize_compiles_other_codes(oracle, N, K, crc, systematic):
     _host_plan(oracle, N, K, crc=crc, systematic=systematic).specialize()
 
 
+def test_specialize_compiles_list_plan(oracle):
+    """Float list plans: the lane-serial kernel with the plan's layout and constants."""
+    p = _host_plan(oracle, 128, 64, L=4, crc=16)
+    assert p.kernel_name() == "sclls_kernel<4>"
+    p.specialize()
+    assert p.kernel_name() == "scl_rtc_kernel"
+
+
 def test_specialize_unsupported_plans(oracle):
     from antpolarcodes_amd._native import PcgError, PCG_E_UNSUPPORTED
-    for kw in ({"L": 8}, {"fixed": True}):
+    for kw in ({"fixed": True}, {"fixed": True, "L": 8}):
         with pytest.raises(PcgError) as e:
             _host_plan(oracle, 256, 128, **kw).specialize()
         assert e.value.code == PCG_E_UNSUPPORTED
