@@ -249,10 +249,12 @@ const char* pcg_plan_kernel_name(const pcg_plan* plan);
  * compile-time schedule -- the same device code and arithmetic as the interpreter kernel, so
  * the same outputs bit for bit.  This replaces the reference's per-code decoder object tree
  * (FastSscAvx::createDecoder, fastssc_avx_float.cpp:797-896) with per-code machine code.
- * Fast-SSC float plans do this by themselves at their first decode of >= 8192 frames
+ * Plans do this by themselves, in a background thread, from their first decode of >= 8192 frames
  * (PCG_RTC=0 never, PCG_RTC=1 at the first decode of any size).  Takes seconds the first time
  * for a code.  PCG_E_UNSUPPORTED for other plans; on a host-only plan it only compiles.  On
- * failure (e.g. no hiprtc) the plan keeps decoding with the interpreter kernel. */
+ * failure (e.g. no hiprtc) the plan keeps decoding with the interpreter kernel.  Float list
+ * plans specialise too (their layout and constants as literals; PCG_RTC_SCL=0: not), 8-bit
+ * plans do not.  pcg_plan_destroy waits for a background compile still running. */
 int pcg_plan_specialize(pcg_plan* plan);
 
 /* SCL plans: the metric path 0 starts every frame of later decode calls with.  0 (the
