@@ -62,13 +62,14 @@ def test_rtc_node_kinds(oracle):
     assert done > 0
 
 
-def test_rtc_auto_large_batch_config2(oracle):
+def test_rtc_auto_large_batch_config2(oracle, monkeypatch):
     """Config 2 (N=1024, K=512, CRC-8): a batch of >= 8192 frames starts the plan's
     specialisation in the background (the interpreter kernel decodes meanwhile); once it is
     loaded the same batch decodes through it.  Both match the oracle."""
     import torch
     from antpolarcodes_amd import frames
     from antpolarcodes_amd._native import Plan
+    monkeypatch.setenv("PCG_RTC", "2")  # the library default (tests/conftest.py turns it off)
     N, K = 1024, 512
     fr = oracle.frozen_bits_bb(N, K, 0.0)
     llr, _, _ = frames.awgn_frames(N, fr, 8192, 2.0, seed=21, crc=8)
@@ -89,7 +90,7 @@ def test_rtc_auto_large_batch_config2(oracle):
 
 
 @pytest.mark.parametrize("N,K,L,crc,systematic", [(256, 128, 4, 16, True), (1024, 512, 8, 8, True),
-                                                  (512, 256, 6, 32, False)])
+                                                  (512, 256, 6, 32, False), (4096, 2048, 32, 8, True)])
 def test_rtc_list_plans(oracle, N, K, L, crc, systematic):
     """Specialised list plans (scl_rtc_kernel: the lane-serial kernel with the plan's layout and
     constants as literals): info, ok and the ordered path metrics bit-exact."""
@@ -99,8 +100,8 @@ def test_rtc_list_plans(oracle, N, K, L, crc, systematic):
     p = Plan(N, L, fr, systematic=systematic, crc=crc, device=0)
     p.specialize()
     assert p.describe()["specialized"] == 1 and p.kernel_name() == "scl_rtc_kernel"
-    for kind in LLR_KINDS:
-        llr = llr_kinds(rng, 64, N, kind)
+    for kind in LLR_KINDS if N <= 1024 else ("normal", "ints"):
+        llr = llr_kinds(rng, 64 if N <= 1024 else 16, N, kind)
         gi, gok, gm = p.decode_host(llr, want_metrics=True)
         oi, ook, om, _, _ = oracle.scl_decode(N, L, fr, llr, systematic=systematic, crc=crc, paths=True)
         assert np.array_equal(gi, oi), kind
