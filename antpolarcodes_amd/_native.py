@@ -89,6 +89,7 @@ def lib():
         L.pcg_plan_kernel_name.restype = C.c_char_p
         L.pcg_plan_set_initial_metric.argtypes = [P, C.c_float]
         L.pcg_plan_specialize.argtypes = [P]
+        L.pcg_plan_specialize_async.argtypes = [P]
         L.pcg_plan_destroy.argtypes = [P]
         L.pcg_plan_destroy.restype = None
         L.pcg_last_error.restype = C.c_char_p
@@ -181,10 +182,12 @@ class Plan:
         """The decode kernel as rocprofv3 names it (pcg_plan_kernel_name)."""
         return lib().pcg_plan_kernel_name(self._h).decode()
 
-    def specialize(self):
-        """Compile and load the kernel specialised to this plan's code (pcg_plan_specialize,
-        hiprtc; Fast-SSC float plans).  Raises PcgError if that fails or is unsupported."""
-        _check(lib().pcg_plan_specialize(self._h))
+    def specialize(self, wait=True):
+        """Compile (or take from a cache) and load the kernel specialised to this plan's code
+        (pcg_plan_specialize, hiprtc; float Fast-SSC and list plans).  wait=False starts it in
+        the background (pcg_plan_specialize_async).  Raises PcgError if that fails or is
+        unsupported."""
+        _check(lib().pcg_plan_specialize(self._h) if wait else lib().pcg_plan_specialize_async(self._h))
 
     def set_initial_metric(self, m):
         """SCL: initial path-0 metric of later decodes (reference metric carry)."""

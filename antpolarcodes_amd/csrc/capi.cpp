@@ -9,9 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <chrono>
 #include <cstring>
-#include <future>
 #include <string>
 #include <vector>
 
@@ -76,7 +74,8 @@ struct pcg_plan {
     int rtc_state = 0;
     bool walk_latency = false; // an adaptive plan's list stage
     bool rtc_scl = true;       // list plans specialise too (PCG_RTC_SCL=0: not)
-    std::future<std::pair<std::vector<char>, std::string>> rtc_job;
+    bool rtc_probed = false;   // the caches were asked for this plan's code object (mode 2)
+    std::shared_ptr<pcg::RtcJob> rtc_job; // the compile this plan waits for (shared, never joined by destroy)
     std::string rtc_err;
     hipModule_t rtc_mod = nullptr;
     hipFunction_t rtc_fn = nullptr;
@@ -184,41 +183,38 @@ std::string rtc_source(const pcg_plan* p)
                                p->scl_fuse);
 }
 
-// Compile (hiprtc, cached per process and on disk) and, on a device plan, load the plan's
-// specialised kernel -- or, with wait = false, start the compile in the background and load
-// it at a later call once it has finished; on failure the plan keeps the interpreter kernel
-// and remembers why.
-int specialize(pcg_plan* p, bool wait = true)
+// Load the finished job's code object into the plan (a device plan: its module and kernel);
+// on failure the plan keeps the interpreter kernel and remembers why.
+int rtc_load(pcg_plan* p)
 {
-    if (p->rtc_state == 1)
-        return PCG_OK;
-    if (p->rtc_state == -1)
-        return fail(PCG_E_HIP, p->rtc_err);
-    if (p->rtc_state == 0) {
-        p->rtc_job = std::async(std::launch::async, [src = rtc_source(p)] {
-            std::pair<std::vector<char>, std::string> r;
-            if (pcg::rtc_compile(src, &r.first, &r.second) != 0)
-                r.first.clear();
-            return r;
-        });
-        p->rtc_state = 2;
-    }
-    if (!wait && p->rtc_job.wait_for(std::chrono::seconds(0)) != std::future_status::ready)
-        return PCG_OK; // still compiling: the interpreter kernel runs meanwhile
-    auto [code, err] = p->rtc_job.get();
-    if (code.empty()) {
+    std::vector<char> code;
+    std::string err;
+    const int r = pcg::rtc_result(*p->rtc_job, &code, &err);
+    p->rtc_job.reset();
+    if (r != 0) {
         p->rtc_state = -1;
         p->rtc_err = "plan specialisation: " + err;
         return fail(PCG_E_HIP, p->rtc_err);
     }
+    const char* fn = p->host.L == 1 ? "scq_rtc_kernel" : "scl_rtc_kernel";
     if (p->device < 0) { // host-only plan: the source compiles; nothing to load
         p->rtc_state = 0;
-        p->kernel = p->host.L == 1 ? "scq_rtc_kernel" : "scl_rtc_kernel";
+        p->kernel = fn;
         return PCG_OK;
+    }
+    // the code objects are built for the library's architecture: refuse another device
+    hipDeviceProp_t prop{};
+    if (hipGetDeviceProperties(&prop, p->device) == hipSuccess) {
+        const std::string an = prop.gcnArchName, want = pcg::rtc_arch();
+        if (an.compare(0, want.size(), want) != 0 || (an.size() > want.size() && an[want.size()] != ':')) {
+            p->rtc_state = -1;
+            p->rtc_err = "plan specialisation: device architecture " + an + " is not the library's " + want;
+            return fail(PCG_E_UNSUPPORTED, p->rtc_err);
+        }
     }
     hipError_t e = hipModuleLoadData(&p->rtc_mod, code.data());
     if (e == hipSuccess)
-        e = hipModuleGetFunction(&p->rtc_fn, p->rtc_mod, p->host.L == 1 ? "scq_rtc_kernel" : "scl_rtc_kernel");
+        e = hipModuleGetFunction(&p->rtc_fn, p->rtc_mod, fn);
     if (e != hipSuccess) {
         if (p->rtc_mod)
             (void)hipModuleUnload(p->rtc_mod);
@@ -229,8 +225,55 @@ int specialize(pcg_plan* p, bool wait = true)
         return fail(PCG_E_HIP, p->rtc_err);
     }
     p->rtc_state = 1;
-    p->kernel = p->host.L == 1 ? "scq_rtc_kernel" : "scl_rtc_kernel";
+    p->kernel = fn;
     return PCG_OK;
+}
+
+// Start the plan's specialisation (a cached code object makes it finish at once; otherwise
+// hiprtc compiles in a background thread shared by every plan of the code) and, with wait, load
+// it -- or, without, load it only if it is ready (a later call loads it otherwise).
+int specialize(pcg_plan* p, bool wait = true)
+{
+    if (p->rtc_state == 1)
+        return PCG_OK;
+    if (p->rtc_state == -1)
+        return fail(PCG_E_HIP, p->rtc_err);
+    if (p->rtc_state == 0) {
+        p->rtc_job = pcg::rtc_start(rtc_source(p));
+        p->rtc_state = 2;
+    }
+    if (!wait && !pcg::rtc_done(*p->rtc_job))
+        return PCG_OK; // still compiling: the interpreter kernel runs meanwhile
+    return rtc_load(p);
+}
+
+// At a decode of F frames (rtc_mode, DESIGN.md "Plan-specialised kernels"): mode 1 specialises
+// and waits; mode 2 uses a cached code object of the plan's code at once (shipped with the
+// library or compiled before), starts a background compile from the first decode of >=
+// RTC_AUTO_FRAMES frames, and switches once it is ready.
+void auto_specialize(pcg_plan* p, uint64_t F)
+{
+    if (p->rtc_mode == 0 || p->rtc_state == 1 || p->rtc_state == -1 || !rtc_capable(p))
+        return;
+    if (p->rtc_state == 2) {
+        (void)specialize(p, p->rtc_mode == 1);
+        return;
+    }
+    if (p->rtc_mode == 1) {
+        (void)specialize(p, true);
+        return;
+    }
+    if (!p->rtc_probed) {
+        p->rtc_probed = true;
+        if (auto j = pcg::rtc_lookup(rtc_source(p))) {
+            p->rtc_job = j;
+            p->rtc_state = 2;
+            (void)rtc_load(p);
+            return;
+        }
+    }
+    if (F >= RTC_AUTO_FRAMES)
+        (void)specialize(p, false);
 }
 
 // lanes per codeword of an adaptive plan's SCL stage, 0 = list_pow2(L).  Measured on
@@ -332,6 +375,24 @@ int pcg_dev_opprof_fetch(unsigned long long* out128)
     (void)hipMemset(g_prof, 0, 128 * sizeof(unsigned long long));
     return PCG_OK;
 }
+
+// Development aid, not part of include/pcg.h: the cache file name of the plan's specialised
+// kernel (antpolarcodes_amd/rtc_warm.py keeps the shipped cache to the listed codes).
+int pcg_dev_rtc_cache_name(const pcg_plan* p, char* out, size_t n)
+{
+    if (!p || !out || n == 0)
+        return fail(PCG_E_ARG, "null argument");
+    if (p->fast)
+        p = p->fast;
+    if (!rtc_capable(p))
+        return fail(PCG_E_UNSUPPORTED, "no plan-specialised kernel for this plan");
+    const std::string name = pcg::rtc_cache_name(rtc_source(p));
+    snprintf(out, n, "%s", name.c_str());
+    return PCG_OK;
+}
+
+// Development aid, not part of include/pcg.h: hiprtc compiles this process started.
+int pcg_dev_rtc_compiles(void) { return pcg::rtc_compiles(); }
 
 int pcg_device_count(void)
 {
@@ -453,6 +514,12 @@ static int plan_create_impl(pcg_plan** out,
     }
     p->kernel = kernel_name(p->host, p->scl_lp);
     p->walk_latency = walk_latency;
+    if (!fixed && L > 1) {
+        bool nd = false;
+        (void)pcg::sclls_rtc_defines(&nd);
+        if (nd) // a dev build of the list kernel (tools/build_dev_lib.sh -D...)
+            p->dev_overrides |= PCG_DEV_BUILD;
+    }
     if (const char* e = getenv("PCG_RTC_SCL"); e && e[0] == '0') {
         p->rtc_scl = false;
         p->dev_overrides |= PCG_DEV_LAYOUT;
@@ -666,11 +733,12 @@ int pcg_plan_describe(const pcg_plan* p, pcg_plan_desc* d)
                           : (p->host.L == 1 && p->host.sc_kind == 2 ? p->host.scq_q : 0);
     d->dev_overrides = p->dev_overrides | (p->fast ? p->fast->dev_overrides : 0u);
     d->recomputed_stages = p->host.L > 1 && !p->host.fixed ? p->scl_virt : 0u;
-    d->specialized = p->rtc_state == 1 ? 1u : 0u;
+    // (an adaptive plan: its Fast-SSC stage, which pcg_plan_specialize specialises)
+    d->specialized = (p->fast ? p->fast->rtc_state : p->rtc_state) == 1 ? 1u : 0u;
     return PCG_OK;
 }
 
-int pcg_plan_specialize(pcg_plan* p)
+static int plan_specialize(pcg_plan* p, bool wait)
 {
     if (!p)
         return fail(PCG_E_ARG, "null plan");
@@ -680,12 +748,16 @@ int pcg_plan_specialize(pcg_plan* p)
         return fail(PCG_E_UNSUPPORTED, "no plan-specialised kernel for this plan (float Fast-SSC and list "
                                        "plans; not the 8-bit decoders, not with PCG_OPPROF)");
     if (p->device < 0)
-        return specialize(p);
+        return specialize(p, wait);
     DeviceGuard g(p->device);
     if (!g.ok)
         return fail(PCG_E_HIP, "hipSetDevice failed");
-    return specialize(p);
+    return specialize(p, wait);
 }
+
+int pcg_plan_specialize(pcg_plan* p) { return plan_specialize(p, true); }
+
+int pcg_plan_specialize_async(pcg_plan* p) { return plan_specialize(p, false); }
 
 static int decode_impl(pcg_plan* p,
                        const float* llr,
@@ -830,10 +902,7 @@ static int decode_impl(pcg_plan* p,
         a.units = (uint32_t)pcg::wave_units(F, 64 / h.scq_q, p->wave_cap);
         a.ops = p->d_ops + h.ops.size(); // the fused schedule (plan.cpp fuse_sc16)
         a.nops = (uint32_t)h.ops_fused.size();
-        if ((p->rtc_state == 0 && rtc_capable(p) &&
-             (p->rtc_mode == 1 || (p->rtc_mode == 2 && F >= RTC_AUTO_FRAMES))) ||
-            p->rtc_state == 2)
-            (void)specialize(p, p->rtc_mode == 1); // on failure the interpreter runs (rtc_err says why)
+        auto_specialize(p, F); // on failure the interpreter runs (rtc_err says why)
         rc = p->rtc_state == 1 ? pcg::rtc_launch(p->rtc_fn, a, s) : pcg::launch_scq(a, h.scq_q, h.scq_virt != 0, s);
     } else if (h.L == 1 && h.sc_kind == 0) {
         a.units = (uint32_t)pcg::wave_units(F, 64, p->wave_cap);
@@ -855,10 +924,7 @@ static int decode_impl(pcg_plan* p,
             if (e != hipSuccess)
                 return hip_fail(e, "hipMemsetAsync(work queue)");
         }
-        if ((p->rtc_state == 0 && rtc_capable(p) &&
-             (p->rtc_mode == 1 || (p->rtc_mode == 2 && F >= RTC_AUTO_FRAMES))) ||
-            p->rtc_state == 2)
-            (void)specialize(p, p->rtc_mode == 1);
+        auto_specialize(p, F);
         rc = p->rtc_state == 1 ? pcg::rtc_launch(p->rtc_fn, a, s) : pcg::launch_sclls(a, s);
     }
     if (rc != 0)
@@ -1050,30 +1116,36 @@ int pcg_decode_f32_soft_host(pcg_plan* p, const float* llr, uint64_t F, uint8_t*
     // the null-stream copies below are ordered after the plan's previous decode
     if ((rc = order_on(p, nullptr)) != 0)
         return rc;
+    // (the shared LLR / info / ok staging grows to F when smaller; the soft buffer follows the
+    // largest soft call alone, so a single frame after a large host batch costs N floats)
     if (p->stage_frames < F || p->soft_frames < F) {
         if ((e = hipStreamSynchronize(nullptr)) != hipSuccess)
             return hip_fail(e, "hipStreamSynchronize");
-        const uint64_t n = std::max(F, p->stage_frames);
+    }
+    if (p->stage_frames < F) {
         (void)hipFree(p->d_llr);
         (void)hipFree(p->d_info);
         (void)hipFree(p->d_ok);
         (void)hipFree(p->d_met);
-        (void)hipFree(p->d_soft);
         p->d_llr = nullptr;
         p->d_info = nullptr;
         p->d_ok = nullptr;
         p->d_met = nullptr;
-        p->d_soft = nullptr;
         p->stage_frames = 0;
-        p->soft_frames = 0;
-        if ((e = hipMalloc(&p->d_llr, n * N * sizeof(float))) != hipSuccess ||
-            (e = hipMalloc(&p->d_info, n * std::max<uint64_t>(kb, 1))) != hipSuccess ||
-            (e = hipMalloc(&p->d_ok, n)) != hipSuccess ||
-            (e = hipMalloc(&p->d_met, n * p->host.L * sizeof(float))) != hipSuccess ||
-            (e = hipMalloc(&p->d_soft, n * N * sizeof(float))) != hipSuccess)
+        if ((e = hipMalloc(&p->d_llr, F * N * sizeof(float))) != hipSuccess ||
+            (e = hipMalloc(&p->d_info, F * std::max<uint64_t>(kb, 1))) != hipSuccess ||
+            (e = hipMalloc(&p->d_ok, F)) != hipSuccess ||
+            (e = hipMalloc(&p->d_met, F * p->host.L * sizeof(float))) != hipSuccess)
             return hip_fail(e, "hipMalloc(soft staging)");
-        p->stage_frames = n;
-        p->soft_frames = n;
+        p->stage_frames = F;
+    }
+    if (p->soft_frames < F) {
+        (void)hipFree(p->d_soft);
+        p->d_soft = nullptr;
+        p->soft_frames = 0;
+        if ((e = hipMalloc(&p->d_soft, F * N * sizeof(float))) != hipSuccess)
+            return hip_fail(e, "hipMalloc(soft codewords)");
+        p->soft_frames = F;
     }
     if ((e = hipMemcpy(p->d_llr, llr, F * N * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
         return hip_fail(e, "hipMemcpy(H2D)");

@@ -40,6 +40,8 @@
 #ifndef PCG_RTC
 #include <stdio.h>
 #include <stdlib.h>
+
+#include <string>
 #endif
 
 namespace pcg {
@@ -685,9 +687,41 @@ PCG_DEV void ls_fgf(Src src, Dst1 d1, Dst2 d2, const DBits& lb, uint32_t s, cons
 // their region holds the channel chunks of m output chunks for every codeword of the
 // wave: one DMA instruction per 1 KB and one wait per round, instead of one dependent
 // register round trip per output chunk (these ops were ~22 % of SCL-8's cycles).
-// Staged image: codeword g, output chunk u, source k at chunk g*8m + 8u + k; k < 4 are
+// Staged image: codeword g, output chunk u, source k at chunk stg_idx(8u + k, g); k < 4 are
 // the channel chunks a_k (alpha[s] chunks c2, c2+hq, c2+hq2, c2+hq2+hq), k >= 4 the
 // chunks a_k + N/8 (their partners y_j+N/2).
+//
+// Codeword-minor order (PCG_STG_GM, default): chunk i of codeword g at i*G + g, so the
+// wave's read of one staged chunk -- every lane of a codeword the same address, the G
+// codewords adjacent 16-byte chunks -- touches G*16 contiguous bytes: no LDS bank conflict.
+// Codeword-major (i + g*per) puts the G addresses per*16 = a multiple of 128 B apart, i.e.
+// on the same banks.  The DMA side is free to use either order: each lane computes its own
+// source address for the LDS slot it fills.
+#ifndef PCG_STG_GM
+#define PCG_STG_GM 1
+#endif
+template <int LP>
+PCG_DEV uint32_t stg_idx(uint32_t i, uint32_t g, uint32_t per)
+{
+#if PCG_STG_GM
+    (void)per;
+    return i * (64u / LP) + g;
+#else
+    return g * per + i;
+#endif
+}
+// the (codeword, chunk) a staging slot f receives
+template <int LP>
+PCG_DEV void stg_slot(uint32_t f, uint32_t per, uint32_t& g, uint32_t& i)
+{
+#if PCG_STG_GM
+    g = f % (64u / LP);
+    i = f / (64u / LP);
+#else
+    g = f / per;
+    i = f % per;
+#endif
+}
 template <int OPC, bool LEFT, int LP, typename Dst2>
 PCG_DEV void ls_fgf_root(const Ls<LP>& c, GlSt d1, Dst2 d2, const DBits& lb, const DBits& rb, uint32_t s,
                          const Share& w, uint32_t m)
@@ -698,7 +732,8 @@ PCG_DEV void ls_fgf_root(const Ls<LP>& c, GlSt d1, Dst2 d2, const DBits& lb, con
     const uint32_t ninst = (64u / LP) * per / 64u; // DMA instructions per round
     const uint32_t n = m / w.h;                 // output chunks per lane per round
     const uint64_t yp = (uint64_t)(uintptr_t)c.y;
-    const float4* mine = reinterpret_cast<const float4*>(stg) + (c.lane / LP) * per;
+    const float4* stg4 = reinterpret_cast<const float4*>(stg);
+    const uint32_t mg = c.lane / LP;
     // s >= 7: the bits of 8 aligned output chunks are one word per source (the root's left
     // half for a right child, the op's own G bits), loaded per 8 chunks -- the first ones
     // while the DMA runs
@@ -720,7 +755,9 @@ PCG_DEV void ls_fgf_root(const Ls<LP>& c, GlSt d1, Dst2 d2, const DBits& lb, con
         __builtin_amdgcn_wave_barrier();
         for (uint32_t t = 0; t < ninst; ++t) {
             const uint32_t f = t * 64u + c.lane;
-            const uint32_t g = f / per, rem = f % per, u = rem >> 3, k = rem & 7u;
+            uint32_t g, rem;
+            stg_slot<LP>(f, per, g, rem);
+            const uint32_t u = rem >> 3, k = rem & 7u;
             uint32_t a = r + u + ((k & 1u) ? hq : 0u) + ((k & 2u) ? hq2 : 0u);
             if (k & 4u)
                 a += hq1;
@@ -742,7 +779,7 @@ PCG_DEV void ls_fgf_root(const Ls<LP>& c, GlSt d1, Dst2 d2, const DBits& lb, con
             float4 yv[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k)
-                yv[k] = mine[u * 8u + k];
+                yv[k] = stg4[stg_idx<LP>(u * 8u + k, mg, per)];
             float4 x[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -810,7 +847,8 @@ PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, co
     const uint32_t ninst = (64u / LP) * per / 64u; // DMA instructions per round
     const uint32_t n = m / w.h;                    // output chunks per lane per round
     const uint64_t yp = (uint64_t)(uintptr_t)c.y;
-    const float4* mine = reinterpret_cast<const float4*>(stg) + (c.lane / LP) * per;
+    const float4* stg4 = reinterpret_cast<const float4*>(stg);
+    const uint32_t mg = c.lane / LP;
     auto koff = [&](uint32_t k) { return ((k & 1u) ? hq : 0u) + ((k & 2u) ? hq2 : 0u); };
     // bit words of 8 aligned output chunks (s >= 7: every offset a multiple of 8 chunks):
     // level l's J >> l outputs at bw[k][J - (J >> (l-1)) + i]
@@ -849,7 +887,9 @@ PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, co
         __builtin_amdgcn_wave_barrier();
         for (uint32_t t = 0; t < ninst; ++t) {
             const uint32_t f = t * 64u + c.lane;
-            const uint32_t g = f / per, rem = f % per, u = rem / (KS * J), k = (rem / J) % KS, j = rem % J;
+            uint32_t g, rem;
+            stg_slot<LP>(f, per, g, rem);
+            const uint32_t u = rem / (KS * J), k = (rem / J) % KS, j = rem % J;
             uint32_t a = r + u + koff(k);
 #pragma unroll
             for (int l = 1; l <= V; ++l)
@@ -875,7 +915,7 @@ PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, co
                 float4 v[J];
 #pragma unroll
                 for (uint32_t j = 0; j < J; ++j)
-                    v[j] = mine[(u * KS + k) * J + j];
+                    v[j] = stg4[stg_idx<LP>((u * KS + k) * J + j, mg, per)];
 #pragma unroll
                 for (int l = 1; l <= V; ++l)
 #pragma unroll
@@ -2313,12 +2353,24 @@ PCG_DEV void sclls_body(const KernelArgs& a)
 #endif
 }
 
+// Translation units (not hiprtc): the host part -- layout, occupancy, dispatch -- is the object
+// built without PCG_LS_INST; each list width's kernel is its own object (Makefile:
+// -DPCG_LS_INST=<LP>), so the five instantiations compile in parallel.  A dev build
+// (tools/build_dev_lib.sh) compiles one width together with the host part (-DPCG_LS_HOST).
 #ifndef PCG_RTC
+#ifndef PCG_LS_INST
+#define PCG_LS_INST 0
+#endif
+#if PCG_LS_INST == 0 && !defined(PCG_LS_HOST)
+#define PCG_LS_HOST 1
+#endif
+#if PCG_LS_INST
 template <int LP>
 __global__ void __launch_bounds__(64, PCG_LS_MINW) sclls_kernel(KernelArgs a)
 {
     sclls_body<LP>(a);
 }
+#endif
 #endif
 
 } // namespace
@@ -2346,6 +2398,34 @@ extern "C" __global__ void __launch_bounds__(64, PCG_LS_MINW) scl_rtc_kernel(Ker
 }
 #else // host side: layout, occupancy, launch
 
+#define PCG_LS_CAT2(x, y) x##y
+#define PCG_LS_CAT(x, y) PCG_LS_CAT2(x, y)
+// per-width entry points of the kernel objects: resident waves per CU at an LDS size, launch
+#define PCG_LS_DECL(W)                                                                                    \
+    int PCG_LS_CAT(sclls_resident_, W)(uint32_t lds_bytes);                                               \
+    int PCG_LS_CAT(sclls_launch_, W)(const KernelArgs& a, size_t lds, hipStream_t stream);
+PCG_LS_DECL(2)
+PCG_LS_DECL(4)
+PCG_LS_DECL(8)
+PCG_LS_DECL(16)
+PCG_LS_DECL(32)
+
+#if PCG_LS_INST
+int PCG_LS_CAT(sclls_resident_, PCG_LS_INST)(uint32_t lds_bytes)
+{
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, sclls_kernel<PCG_LS_INST>, 64, lds_bytes) != hipSuccess)
+        n = 0;
+    return n;
+}
+int PCG_LS_CAT(sclls_launch_, PCG_LS_INST)(const KernelArgs& a, size_t lds, hipStream_t stream)
+{
+    hipLaunchKernelGGL(sclls_kernel<PCG_LS_INST>, dim3(a.units), dim3(64), lds, stream, a);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+#endif
+
+#ifdef PCG_LS_HOST
 #ifndef PCG_SCL_VIRT_DEFAULT
 #define PCG_SCL_VIRT_DEFAULT 3 // recomputed top stages (2: the quarters too, 3: eighths for LP >= 16, where sclls_layout allows)
 #endif
@@ -2436,21 +2516,41 @@ int sclls_layout(uint32_t N, uint32_t L, uint32_t lp, uint32_t vleaf, uint32_t* 
     return 0;
 }
 
+std::string sclls_rtc_defines(bool* nondefault)
+{
+    // (the knobs' values in this translation unit: a dev build's -D flags reach the hiprtc
+    // source too, so its specialised kernel is the variant's, with the layout computed here)
+    std::string s;
+    bool nd = false;
+    auto d = [&](const char* k, long v, long dflt) {
+        s += std::string("#define ") + k + " " + std::to_string(v) + "\n";
+        nd = nd || v != dflt;
+    };
+    d("PCG_LS_DBITS_LP", PCG_LS_DBITS_LP, 16);
+    d("PCG_FGF_U", PCG_FGF_U, 1);
+    d("PCG_STG_GM", PCG_STG_GM, 1);
+    d("PCG_SEL_BITONIC_LP", PCG_SEL_BITONIC_LP, 16);
+    d("PCG_SEL_BITONIC_K", PCG_SEL_BITONIC_K, 4);
+    d("PCG_LS_MINW", PCG_LS_MINW, 2);
+#ifdef PCG_LS_FULL_LOCAL_SORT
+    s += "#define PCG_LS_FULL_LOCAL_SORT 1\n";
+    nd = true;
+#endif
+#ifdef PCG_LS_PROF
+    s += "#define PCG_LS_PROF 1\n";
+    nd = true;
+#endif
+    if (nondefault)
+        *nondefault = nd;
+    return s;
+}
+
 static uint32_t lp_of(uint32_t L)
 {
     uint32_t lp = 2;
     while (lp < L)
         lp <<= 1;
     return lp;
-}
-
-template <int LP>
-static int ls_resident(uint32_t lds_bytes)
-{
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, sclls_kernel<LP>, 64, lds_bytes) != hipSuccess)
-        n = 0;
-    return n;
 }
 
 // Waves (= scratch units) for a launch of F frames: one persistent wave per resident
@@ -2462,17 +2562,13 @@ uint64_t sclls_wave_cap(uint32_t lp, uint32_t wave_lds_floats)
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const uint32_t lds = wave_lds_floats * 4u;
     int res = 0;
-#ifdef PCG_LS_ONLY // dev builds: one instantiation (compile time)
-    res = lp == PCG_LS_ONLY ? ls_resident<PCG_LS_ONLY>(lds) : 0;
-#else
     switch (lp) {
-    case 2: res = ls_resident<2>(lds); break;
-    case 4: res = ls_resident<4>(lds); break;
-    case 8: res = ls_resident<8>(lds); break;
-    case 16: res = ls_resident<16>(lds); break;
-    default: res = ls_resident<32>(lds); break;
+    case 2: res = sclls_resident_2(lds); break;
+    case 4: res = sclls_resident_4(lds); break;
+    case 8: res = sclls_resident_8(lds); break;
+    case 16: res = sclls_resident_16(lds); break;
+    default: res = sclls_resident_32(lds); break;
     }
-#endif
     uint64_t wpc = res > 0 ? (uint64_t)res : 1;
     if (wpc > 8)
         wpc = 8;
@@ -2493,23 +2589,17 @@ int launch_sclls(const KernelArgs& a, hipStream_t stream)
     lds += 64 * sizeof(uint64_t);
 #endif
     const uint32_t lp = a.scl_lp > lp_of(a.L) ? a.scl_lp : lp_of(a.L);
-#ifdef PCG_LS_ONLY
-    if (lp != PCG_LS_ONLY)
-        return -4;
-    hipLaunchKernelGGL(sclls_kernel<PCG_LS_ONLY>, dim3((uint32_t)grid), dim3(64), lds, stream, a);
-#else
     switch (lp) {
-    case 2: hipLaunchKernelGGL(sclls_kernel<2>, dim3((uint32_t)grid), dim3(64), lds, stream, a); break;
-    case 4: hipLaunchKernelGGL(sclls_kernel<4>, dim3((uint32_t)grid), dim3(64), lds, stream, a); break;
-    case 8: hipLaunchKernelGGL(sclls_kernel<8>, dim3((uint32_t)grid), dim3(64), lds, stream, a); break;
-    case 16: hipLaunchKernelGGL(sclls_kernel<16>, dim3((uint32_t)grid), dim3(64), lds, stream, a); break;
-    case 32: hipLaunchKernelGGL(sclls_kernel<32>, dim3((uint32_t)grid), dim3(64), lds, stream, a); break;
+    case 2: return sclls_launch_2(a, lds, stream);
+    case 4: return sclls_launch_4(a, lds, stream);
+    case 8: return sclls_launch_8(a, lds, stream);
+    case 16: return sclls_launch_16(a, lds, stream);
+    case 32: return sclls_launch_32(a, lds, stream);
     default: return -4;
     }
-#endif
-    return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+#endif // PCG_LS_HOST
 #endif // PCG_RTC
 
 } // namespace pcg

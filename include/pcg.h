@@ -106,7 +106,8 @@ typedef struct pcg_plan_desc {
     uint32_t recomputed_stages;  /* lane-serial SCL: top LLR stages recomputed from the channel
                                     where read instead of stored (1: the root's children, 2:
                                     also its grandchildren); 0 for the other kernels */
-    uint32_t specialized;        /* 1: decodes run the plan-specialised kernel (pcg_plan_specialize) */
+    uint32_t specialized;        /* 1: decodes run the plan-specialised kernel (pcg_plan_specialize;
+                                    an adaptive plan: its Fast-SSC stage) */
 } pcg_plan_desc;
 
 #define PCG_DEV_SCL_LP 0x1   /* PCG_SCL_LP / PCG_ADAPT_LP (only when the caller passed 0) */
@@ -115,6 +116,7 @@ typedef struct pcg_plan_desc {
 #define PCG_DEV_LAYOUT 0x8   /* PCG_SC_KERNEL, PCG_*_LDS_KB, PCG_*_SL, PCG_*_WPC, PCG_SCL_VIRT, ... */
 #define PCG_DEV_OPPROF 0x10  /* PCG_OPPROF */
 #define PCG_DEV_FLAGS 0x20   /* PCG_FLAGS */
+#define PCG_DEV_BUILD 0x40   /* a development build of the list kernel (compile-time knobs != defaults) */
 
 /* Build a decoding plan: classify the decoder tree exactly as the reference
  * (Fast-SSC for L == 1, SCL for L >= 2), flatten it to a device schedule and
@@ -244,18 +246,27 @@ int pcg_plan_describe(const pcg_plan* plan, pcg_plan_desc* desc);
  * "scs_kernel"), as it appears in rocprofv3 kernel traces; "" for NULL. */
 const char* pcg_plan_kernel_name(const pcg_plan* plan);
 
-/* Compile (hiprtc, at run time, cached per process and code) and load a kernel specialised
- * to this plan's code: the LDS-resident Fast-SSC kernel with the plan's decoder tree as a
- * compile-time schedule -- the same device code and arithmetic as the interpreter kernel, so
- * the same outputs bit for bit.  This replaces the reference's per-code decoder object tree
- * (FastSscAvx::createDecoder, fastssc_avx_float.cpp:797-896) with per-code machine code.
- * Plans do this by themselves, in a background thread, from their first decode of >= 8192 frames
- * (PCG_RTC=0 never, PCG_RTC=1 at the first decode of any size).  Takes seconds the first time
- * for a code.  PCG_E_UNSUPPORTED for other plans; on a host-only plan it only compiles.  On
- * failure (e.g. no hiprtc) the plan keeps decoding with the interpreter kernel.  Float list
- * plans specialise too (their layout and constants as literals; PCG_RTC_SCL=0: not), 8-bit
- * plans do not.  pcg_plan_destroy waits for a background compile still running. */
+/* Compile (hiprtc, at run time) and load a kernel specialised to this plan's code: the
+ * LDS-resident Fast-SSC kernel with the plan's decoder tree as a compile-time schedule, or the
+ * lane-serial list kernel with the plan's layout and constants as literals -- the same device
+ * code and arithmetic as the interpreter kernels, so the same outputs bit for bit.  This
+ * replaces the reference's per-code decoder object tree (FastSscAvx::createDecoder,
+ * fastssc_avx_float.cpp:797-896; SclAvx::createDecoder, scl_avx_float.cpp:624-651) with
+ * per-code machine code.  Code objects are cached per process, in the library's shipped
+ * cache (<dir of libpcg.so>/rtc, filled at build time for the benchmark and test codes) and
+ * on disk (PCG_RTC_CACHE); a code in none of them takes tens of seconds of hiprtc once.
+ * Plans do this by themselves: with a cached code object from their first decode, otherwise
+ * in a background thread from their first decode of >= 8192 frames, switching once it is
+ * ready (PCG_RTC=0 never, PCG_RTC=1 at the first decode, waiting).  PCG_E_UNSUPPORTED for
+ * 8-bit plans (and with PCG_OPPROF); on a host-only plan it only compiles.  On failure (no
+ * hiprtc, a device of another architecture) the plan keeps decoding with the interpreter
+ * kernel.  Plans of one code share one compile; pcg_plan_destroy never waits for it (process
+ * exit does). */
 int pcg_plan_specialize(pcg_plan* plan);
+
+/* Start pcg_plan_specialize without waiting: the plan switches at a later decode (or
+ * pcg_plan_specialize) once the code object is ready.  Returns at once. */
+int pcg_plan_specialize_async(pcg_plan* plan);
 
 /* SCL plans: the metric path 0 starts every frame of later decode calls with.  0 (the
  * default) is a freshly constructed reference decoder; passing the previous frame's final

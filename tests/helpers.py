@@ -60,3 +60,24 @@ def reference_digest(name):
     import os
     with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "reference_digests.json")) as fh:
         return json.load(fh)["cases"][name]
+
+
+KERNELS = ("interp", "rtc")
+
+
+def gpu_plan(N, L, frozen, kernel="interp", device=0, **kw):
+    """A device plan on the interpreter kernel ("interp": tests/conftest.py keeps plans from
+    specialising themselves) or on its plan-specialised kernel ("rtc": pcg_plan_specialize,
+    loaded from the library's shipped cache for the test codes, antpolarcodes_amd/rtc_warm.py).
+    Asserts which kernel the decodes will launch."""
+    from antpolarcodes_amd._native import Plan
+    p = Plan(N, L, frozen, device=device, **kw)
+    if kernel == "rtc":
+        p.specialize()
+        assert p.describe()["specialized"] == 1
+        if not kw.get("adaptive"):  # (an adaptive plan names its list stage's kernel)
+            want = "scq_rtc_kernel" if L == 1 else "scl_rtc_kernel"
+            assert p.kernel_name() == want, p.kernel_name()
+    else:
+        assert p.describe()["specialized"] == 0 and "rtc" not in p.kernel_name(), p.kernel_name()
+    return p

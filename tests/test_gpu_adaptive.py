@@ -17,15 +17,19 @@ def _expect(oracle, N, L, fr, llr, crc, systematic=True):
     return info, ok, met, use_scl
 
 
+@pytest.mark.parametrize("kernel", ["interp", "rtc"])
 @pytest.mark.parametrize("ebn0", [1.0, 2.5])
 @pytest.mark.parametrize("crc", [8, 16, 32])
-def test_adaptive_matches_oracle(oracle, ebn0, crc):
+def test_adaptive_matches_oracle(oracle, ebn0, crc, kernel):
+    """AdaptiveFloat frame by frame; "rtc": its Fast-SSC stage on the plan-specialised kernel
+    (what the library runs for the code; the list stage, a few frames per call, stays on the
+    interpreter walk)."""
     from antpolarcodes_amd import frames
-    from antpolarcodes_amd._native import Plan
+    from helpers import gpu_plan
     N, L = 1024, 8
     fr = oracle.frozen_bits_bb(N, 512, 0.0)
     llr, _, _ = frames.awgn_frames(N, fr, 3000, ebn0, seed=crc, crc=crc)
-    p = Plan(N, L, fr, crc=crc, device=0, adaptive=True)
+    p = gpu_plan(N, L, fr, kernel, crc=crc, adaptive=True)
     gi, gok, gm = p.decode_host(llr, want_metrics=True)
     ei, eok, em, use_scl = _expect(oracle, N, L, fr, llr, crc)
     assert 0 < use_scl.sum() < len(use_scl)

@@ -62,15 +62,19 @@ def test_device_depuncture_batch_matches_oracle(oracle):
     assert np.array_equal(out.cpu().numpy().view(np.uint32), oracle.depuncture(896, fr, llr).view(np.uint32))
 
 
+@pytest.mark.parametrize("kernel", ["interp", "rtc"])
 @pytest.mark.parametrize("L", [1, 8])
-def test_decode_punctured_matches_oracle(oracle, L):
-    """Config 4: FiveGList(1024, 512), CRC-11, E = 896 -> depuncture + decode on the GPU."""
+def test_decode_punctured_matches_oracle(oracle, L, kernel):
+    """Config 4: FiveGList(1024, 512), CRC-11, E = 896 -> depuncture + decode on the GPU, on
+    the interpreter and on the plan-specialised kernel the bench runs (exact +0.0 LLRs of the
+    punctured positions: certain SCL sort ties, scl_avx_float.cpp:316-621)."""
     import torch
     from antpolarcodes_amd import frames
-    from antpolarcodes_amd._native import Plan, Puncturer
+    from antpolarcodes_amd._native import Puncturer
+    from helpers import gpu_plan
     F = 2048 if L > 1 else 8192
     llr, info_tx, fr, _ = frames.nr_frames(896, 512, F, 1.25, seed=40 + L)
-    plan = Plan(1024, L, fr, systematic=True, crc=11, device=0)
+    plan = gpu_plan(1024, L, fr, kernel, systematic=True, crc=11)
     punc = Puncturer(896, fr, device=0)
     d_info = torch.empty((F, 64), dtype=torch.uint8, device="cuda:0")
     d_ok = torch.empty(F, dtype=torch.uint8, device="cuda:0")
@@ -96,7 +100,7 @@ def test_decode_punctured_matches_oracle(oracle, L):
         from helpers import reference_digest, sha256
         d = reference_digest("config4_nr_scl8")
         assert sha256(d_met.cpu().numpy()) == d["metrics"]
-        p0 = Plan(1024, 8, fr, systematic=True, crc=0, device=0)
+        p0 = gpu_plan(1024, 8, fr, kernel, systematic=True, crc=0)
         d0 = torch.empty((F, 64), dtype=torch.uint8, device="cuda:0")
         k0 = torch.empty(F, dtype=torch.uint8, device="cuda:0")
         p0.decode_punctured_device(punc, _t(llr), d0, k0)

@@ -89,14 +89,19 @@ def test_rtc_auto_large_batch_config2(oracle, monkeypatch):
         assert p.kernel_name() == "scq_rtc_kernel"
 
 
-@pytest.mark.parametrize("N,K,L,crc,systematic", [(256, 128, 4, 16, True), (1024, 512, 8, 8, True),
-                                                  (512, 256, 6, 32, False), (4096, 2048, 32, 8, True)])
-def test_rtc_list_plans(oracle, N, K, L, crc, systematic):
+@pytest.mark.parametrize("N,K,L,crc,systematic,kind", [
+    (256, 128, 4, 16, True, "BB"), (1024, 512, 8, 8, True, "BB"), (512, 256, 6, 32, False, "BB"),
+    (4096, 2048, 32, 8, True, "BB"), (1024, 512, 12, 8, True, "BB"), (1024, 512, 8, 0, True, "BB"),
+    (1024, 512, 8, 11, True, "5G"), (1024, 512, 8, 0, True, "5G")])
+def test_rtc_list_plans(oracle, N, K, L, crc, systematic, kind):
     """Specialised list plans (scl_rtc_kernel: the lane-serial kernel with the plan's layout and
-    constants as literals): info, ok and the ordered path metrics bit-exact."""
+    constants as literals): info, ok and the ordered path metrics bit-exact -- BB codes, a list
+    size that is not a power of two, no detector, and config 4's 5G reliability-list code with
+    CRC-11 and with the Dummy detector."""
     from antpolarcodes_amd._native import Plan
+    from antpolarcodes_amd.construction import frozen_bits
     rng = np.random.default_rng(N + L)
-    fr = oracle.frozen_bits_bb(N, K, 0.0)
+    fr = oracle.frozen_bits_bb(N, K, 0.0) if kind == "BB" else frozen_bits(N, K, 0.0, "5G")
     p = Plan(N, L, fr, systematic=systematic, crc=crc, device=0)
     p.specialize()
     assert p.describe()["specialized"] == 1 and p.kernel_name() == "scl_rtc_kernel"
@@ -107,3 +112,36 @@ def test_rtc_list_plans(oracle, N, K, L, crc, systematic):
         assert np.array_equal(gi, oi), kind
         assert np.array_equal(gok, ook), kind
         assert np.array_equal(gm.view(np.uint32), om.view(np.uint32)), kind
+
+
+def test_rtc_default_mode_list_plan(oracle, monkeypatch):
+    """The library default (PCG_RTC=2) on list plans: a code whose specialised kernel is in the
+    shipped cache (config 3) runs it from its first decode; a code that is not (N=1024 K=600
+    L=4) decodes on the interpreter while its compile runs in the background (started by a
+    batch of >= 8192 frames) and switches once it is loaded.  Every output matches the oracle."""
+    import torch
+    from antpolarcodes_amd import frames
+    from antpolarcodes_amd._native import Plan
+    monkeypatch.setenv("PCG_RTC", "2")
+    fr = oracle.frozen_bits_bb(1024, 512, 0.0)
+    llr, _, _ = frames.awgn_frames(1024, fr, 64, 1.5, seed=3, crc=8)
+    p = Plan(1024, 8, fr, crc=8, device=0)
+    gi, gok, gm = p.decode_host(llr, want_metrics=True)
+    assert p.kernel_name() == "scl_rtc_kernel"
+    oi, ook, om, _, _ = oracle.scl_decode(1024, 8, fr, llr, crc=8, paths=True)
+    assert np.array_equal(gi, oi) and np.array_equal(gok, ook)
+    assert np.array_equal(gm.view(np.uint32), om.view(np.uint32))
+    fr = oracle.frozen_bits_bb(1024, 600, 0.0)
+    llr, _, _ = frames.awgn_frames(1024, fr, 8192, 2.5, seed=4, crc=16)
+    x = torch.from_numpy(llr).cuda()
+    oi, ook = oracle.scl_decode(1024, 4, fr, llr[:1024], crc=16)
+    q = Plan(1024, 4, fr, crc=16, device=0)
+    for rnd in range(2):
+        info = torch.zeros((8192, q.kb), dtype=torch.uint8, device="cuda")
+        ok = torch.zeros(8192, dtype=torch.uint8, device="cuda")
+        q.decode_device(x, info, ok)
+        torch.cuda.synchronize()
+        assert np.array_equal(info[:1024].cpu().numpy(), oi), q.kernel_name()
+        assert np.array_equal(ok[:1024].cpu().numpy(), ook), q.kernel_name()
+        q.specialize()  # waits for the background compile
+        assert q.kernel_name() == "scl_rtc_kernel"

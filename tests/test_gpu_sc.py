@@ -5,7 +5,7 @@ The oracle (oracle/polar_oracle.c) is pinned to the reference by tests/test_orac
 import numpy as np
 import pytest
 
-from helpers import LLR_KINDS, llr_kinds, node_cover_sets, reference_digest, sha256
+from helpers import KERNELS, LLR_KINDS, gpu_plan, llr_kinds, node_cover_sets, reference_digest, sha256
 
 pytestmark = pytest.mark.gpu
 
@@ -87,16 +87,22 @@ def test_sc_random_frozen_sets(oracle):
     assert tested > 100
 
 
-def test_sc_awgn_batch_config2(oracle):
-    """Config 2 shape: N=1024 K=512 BB(0 dB) AWGN Eb/N0 = 2 dB, 2^16 frames."""
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_sc_awgn_batch_config2(oracle, kernel):
+    """Config 2 shape: N=1024 K=512 BB(0 dB) AWGN Eb/N0 = 2 dB, 2^16 frames, through the
+    interpreter kernel and through the plan-specialised kernel the library and bench run."""
     from antpolarcodes_amd import frames
     fr = _bb(oracle, 1024, 512)
     llr, info, _ = frames.awgn_frames(1024, fr, 1 << 16, 2.0, seed=2, crc=8)
-    _check_sc(oracle, 1024, fr, llr)
+    p = gpu_plan(1024, 1, fr, kernel, crc=8)
+    gi, gok, _ = p.decode_host(llr)
+    oi, ook = oracle.sc_decode(1024, fr, llr, crc=8)
+    bad = np.nonzero(~(gi == oi).all(axis=1))[0]
+    assert bad.size == 0, f"info mismatch in frames {bad[:8]}"
+    assert np.array_equal(gok, ook)
     # ... and the whole batch against the reference itself (tests/golden/make_digests.py)
     d = reference_digest("config2_sc")
     assert sha256(llr) == d["llr"], "frame generator changed: regenerate the digests"
-    gi, gok, _ = _plan(1024, 1, fr).decode_host(llr)
     assert sha256(gi) == d["info"] and sha256(gok) == d["ok"]
 
 

@@ -7,9 +7,11 @@ Oracle semantics: a freshly constructed reference decoder per frame (Q8).
 import numpy as np
 import pytest
 
-from helpers import LLR_KINDS, llr_kinds, reference_digest, sha256
+from helpers import KERNELS, LLR_KINDS, gpu_plan, llr_kinds, reference_digest, sha256
 
 pytestmark = pytest.mark.gpu
+
+_ORACLE = {}  # oracle outputs of the large batches, shared by the kernel parametrizations
 
 
 def _plan(N, L, frozen, systematic=True, crc=8):
@@ -87,31 +89,43 @@ def test_scl_recomputed_top_stages(oracle, monkeypatch, virt, L):
         _check_scl(oracle, N, L, fr, llr, systematic=False)
 
 
-def test_scl_awgn_batch_config3(oracle):
-    """Config 3 shape: SCL L=8, N=1024 K=512, CRC-8, 2^16 AWGN frames at 2 dB."""
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_scl_awgn_batch_config3(oracle, kernel):
+    """Config 3 shape: SCL L=8, N=1024 K=512, CRC-8, 2^16 AWGN frames at 2 dB, through the
+    interpreter and through the plan-specialised kernel (scl_rtc_kernel) the bench runs: every
+    frame's info, ok and ordered path metrics against the oracle and the reference's digest."""
     from antpolarcodes_amd import frames
     fr = oracle.frozen_bits_bb(1024, 512, 0.0)
     llr, info, _ = frames.awgn_frames(1024, fr, 1 << 16, 2.0, seed=4, crc=8)
-    _check_scl(oracle, 1024, 8, fr, llr)
-    _check_digest("config3_scl8", 1024, 8, fr, llr)
+    p = gpu_plan(1024, 8, fr, kernel, crc=8)
+    gi, gok, gm = p.decode_host(llr, want_metrics=True)
+    if "config3" not in _ORACLE:  # (one oracle run serves both kernels)
+        _ORACLE["config3"] = oracle.scl_decode(1024, 8, fr, llr, crc=8, paths=True)
+    oi, ook, om, _, _ = _ORACLE["config3"]
+    bad = np.nonzero(~(gi == oi).all(axis=1))[0]
+    assert bad.size == 0, f"info mismatch in frames {bad[:8]}"
+    assert np.array_equal(gok, ook)
+    assert np.array_equal(gm.view(np.uint32), om.view(np.uint32))
+    _check_digest("config3_scl8", llr, gi, gok, gm)
 
 
-def _check_digest(name, N, L, fr, llr, crc=8):
+def _check_digest(name, llr, gi, gok, gm):
     """The whole batch against the reference itself (tests/golden/make_digests.py)."""
     d = reference_digest(name)
     assert sha256(llr) == d["llr"], "frame generator changed: regenerate the digests"
-    gi, gok, gm = _plan(N, L, fr, crc=crc).decode_host(llr, want_metrics=True)
     assert sha256(gi) == d["info"] and sha256(gok) == d["ok"]
     assert sha256(gm) == d["metrics"]
 
 
-def test_scl32_reference_digest(oracle):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_scl32_reference_digest(oracle, kernel):
     """Config 5's code (N=4096 K=2048 L=32, CRC-8) on 4096 host frames: info, ok and the
-    ordered path metrics of every frame equal the reference's (by digest)."""
+    ordered path metrics of every frame equal the reference's (by digest), on both kernels."""
     from antpolarcodes_amd import frames
     fr = oracle.frozen_bits_bb(4096, 2048, 0.0)
     llr, _, _ = frames.awgn_frames(4096, fr, 4096, 1.5, seed=55, crc=8)
-    _check_digest("config5_scl32", 4096, 32, fr, llr)
+    gi, gok, gm = gpu_plan(4096, 32, fr, kernel, crc=8).decode_host(llr, want_metrics=True)
+    _check_digest("config5_scl32", llr, gi, gok, gm)
 
 
 def test_scl_n4096_l32(oracle):
@@ -122,13 +136,14 @@ def test_scl_n4096_l32(oracle):
     _check_scl(oracle, 4096, 32, fr, llr)
 
 
-def test_scl32_config5_shard(oracle):
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_scl32_config5_shard(oracle, kernel):
     """Config 5 at its per-GPU shard size: 2^17 frames of N=4096 K=2048 SCL-32 (one of the
     8 contiguous shards of the 2^20-frame batch), frames made on the device; a strided subset
     is checked against the oracle (info, ok and path metrics bit for bit), every frame against
     the transmitted information where the CRC passed."""
     import torch
-    from antpolarcodes_amd._native import Encoder, Plan, bpsk_awgn_device, random_info_device
+    from antpolarcodes_amd._native import Encoder, bpsk_awgn_device, random_info_device
     N, K, L, F = 4096, 2048, 32, 1 << 17
     fr = oracle.frozen_bits_bb(N, K, 0.0)
     info = torch.empty((F, K // 8), dtype=torch.uint8, device="cuda:0")
@@ -139,7 +154,7 @@ def test_scl32_config5_shard(oracle):
     esn0 = 10 ** 0.15 * K / N  # Eb/N0 1.5 dB
     bpsk_awgn_device(code, N, float(1 / np.sqrt(2 * esn0)), 23, llr)
     del code
-    p = Plan(N, L, fr, crc=8, device=0)
+    p = gpu_plan(N, L, fr, kernel, crc=8)
     out = torch.empty_like(info)
     ok = torch.empty(F, dtype=torch.uint8, device="cuda:0")
     met = torch.empty((F, L), dtype=torch.float32, device="cuda:0")

@@ -16,15 +16,17 @@ def _host_plan(oracle, N, K, L=1, crc=8, systematic=True, fixed=False):
     return Plan(N, L, oracle.frozen_bits_bb(N, K, 0.0), systematic=systematic, crc=crc, device=-1, fixed=fixed)
 
 
-def test_specialize_compiles_config2(oracle, tmp_path, monkeypatch):
-    p = _host_plan(oracle, 1024, 512)
+def test_specialize_compiles_a_new_code(oracle, tmp_path, monkeypatch):
+    """A code the shipped cache does not hold: compiled once, then from the process cache and,
+    for other processes, the user cache."""
+    p = _host_plan(oracle, 512, 200)
     assert p.kernel_name().startswith("scq_kernel")
     t = time.time()
     p.specialize()
     first = time.time() - t
     assert p.kernel_name() == "scq_rtc_kernel"
     t = time.time()
-    _host_plan(oracle, 1024, 512).specialize()  # same code: the process cache
+    _host_plan(oracle, 512, 200).specialize()  # same code: the process cache
     assert time.time() - t < max(0.5, first / 4)
     files = list((tmp_path / "rtc").glob("pcg_*.co"))  # and the disk cache, for other processes
     assert len(files) == 1 and files[0].read_bytes()[:4] == b"\x7fELF"
@@ -49,3 +51,83 @@ def test_specialize_unsupported_plans(oracle):
         with pytest.raises(PcgError) as e:
             _host_plan(oracle, 256, 128, **kw).specialize()
         assert e.value.code == PCG_E_UNSUPPORTED
+
+
+def _run(code, env_extra, timeout=600):
+    """A fresh process (its own process cache) running `code` with the repo on sys.path."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if not k.startswith("PCG_")}
+    env.update(env_extra)
+    pre = ("import sys, time, ctypes; sys.path.insert(0, %r)\n"
+           "from antpolarcodes_amd._native import Plan, lib\n"
+           "from antpolarcodes_amd.construction import frozen_bits\n" % root)
+    r = subprocess.run([sys.executable, "-c", pre + code], env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return r.stdout
+
+
+# a code no shipped cache holds (antpolarcodes_amd/rtc_warm.py): compiles in a few seconds
+_SMALL = "p = Plan(16, 1, frozen_bits(16, 8, 0.0, 'BB'), systematic=False, crc=0, device=-1)\n"
+
+
+def test_corrupt_or_foreign_cache_files_are_recompiled(tmp_path):
+    """A torn, truncated or foreign file under a cache name is never loaded: the code is
+    compiled again and the file rewritten whole (trailer: magic, length, checksum)."""
+    env = {"PCG_RTC_CACHE": str(tmp_path)}
+    _run(_SMALL + "p.specialize()\n", env)
+    files = list(tmp_path.glob("pcg_*.co"))
+    assert len(files) == 1
+    good = files[0].read_bytes()
+    assert good[:4] == b"\x7fELF" and good[-24:-16] == b"PCGRTC01"
+    for bad in (good[:-30], good[:len(good) // 2], b"\x7fELF" + b"\0" * 4096, good[:-1] + bytes([good[-1] ^ 1])):
+        files[0].write_bytes(bad)
+        out = _run(_SMALL + "p.specialize()\nprint('compiles', lib().pcg_dev_rtc_compiles())\n", env)
+        assert "compiles 1" in out  # recompiled, not loaded
+        assert files[0].read_bytes() == good
+    out = _run(_SMALL + "p.specialize()\nprint('compiles', lib().pcg_dev_rtc_compiles())\n", env)
+    assert "compiles 0" in out  # the valid file is used
+    assert not list(tmp_path.glob(".pcg_*"))  # no temp files left behind
+
+
+def test_destroy_during_compile_and_shared_compile(tmp_path):
+    """Two plans of one code share one hiprtc compile; destroying a plan whose compile is
+    still running returns at once (the detached compile finishes on its own), and the process
+    exits cleanly after it."""
+    code = (_SMALL + "q = Plan(16, 1, frozen_bits(16, 8, 0.0, 'BB'), systematic=False, crc=0, device=-1)\n"
+            "p.specialize(wait=False); q.specialize(wait=False)\n"
+            "t = time.time(); p.close(); dt = time.time() - t\n"
+            "assert dt < 0.5, dt\n"
+            "q.specialize()\n"
+            "assert q.kernel_name() == 'scq_rtc_kernel'\n"
+            "print('compiles', lib().pcg_dev_rtc_compiles())\n"
+            "r = Plan(16, 1, frozen_bits(16, 8, 0.0, 'BB'), systematic=False, crc=0, device=-1)\n"
+            "r.specialize(wait=False); del r\n")  # a finished job: nothing left to wait for at exit
+    out = _run(code, {"PCG_RTC_CACHE": str(tmp_path)})
+    assert "compiles 1" in out
+    # exit while a compile of another code is still running: the process waits for it
+    code = ("p = Plan(32, 1, frozen_bits(32, 16, 0.0, 'BB'), systematic=False, crc=16, device=-1)\n"
+            "p.specialize(wait=False); p.close()\n")
+    _run(code, {"PCG_RTC_CACHE": str(tmp_path / "b")})
+    assert len(list((tmp_path / "b").glob("pcg_*.co"))) == 1
+
+
+def test_shipped_cache_holds_the_benchmark_codes():
+    """The build (antpolarcodes_amd/rtc_warm.py) ships the specialised kernels of the benchmark
+    configurations next to the library: they load without any compile."""
+    code = ("from antpolarcodes_amd.rtc_warm import bench_codes\n"
+            "for N, L, (kind, K), crc, sysm in bench_codes():\n"
+            "    p = Plan(N, L, frozen_bits(N, K, 0.0, kind), systematic=sysm, crc=crc, device=-1)\n"
+            "    p.specialize()\n"
+            "print('compiles', lib().pcg_dev_rtc_compiles())\n")
+    assert "compiles 0" in _run(code, {"PCG_RTC_CACHE": "0"}, timeout=120)
+
+
+def test_dev_build_knobs_reach_the_specialised_source():
+    """The specialised list kernel is compiled with the library's own compile-time knobs
+    (sclls_rtc_defines), and a plan of a default build reports no development override."""
+    code = ("p = Plan(1024, 8, frozen_bits(1024, 512, 0.0, 'BB'), crc=8, device=-1)\n"
+            "print('dev', p.describe()['dev_overrides'])\n")
+    assert "dev 0" in _run(code, {})

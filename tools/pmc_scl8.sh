@@ -23,7 +23,7 @@ out = sys.argv[1]
 agg = collections.defaultdict(list)
 for f in glob.glob(out + "/p*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "sclls_kernel" in r["Kernel_Name"] or "scq_kernel" in r["Kernel_Name"] or "scl_char" in r["Kernel_Name"]:
+        if any(k in r["Kernel_Name"] for k in ("sclls_kernel", "scq_kernel", "scl_char", "rtc_kernel", "sccs_kernel")):
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 with open(out + "/pmc_summary.txt", "w") as fh:
     for k, v in sorted(agg.items()):
