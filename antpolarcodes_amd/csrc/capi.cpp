@@ -28,7 +28,7 @@ struct pcg_plan {
     uint32_t scl_sb = 0;          // lane-serial SCL: bit buffers below this stage in LDS (0: codeword rows)
     uint64_t scratch_floats = 0;  // per scratch unit (lane-serial wave)
     float* d_scratch = nullptr;   // grown stream-ordered (hipMallocAsync) when a launch needs more waves
-    uint64_t scratch_frames = 0;  // capacity in scratch units
+    uint64_t scratch_cap = 0;     // capacity in elements (units x per-unit floats / dwords)
     // persistent-wave caps of this plan's kernel on its device (float / int8 channel input),
     // evaluated once at plan creation
     uint64_t wave_cap = 0;
@@ -308,21 +308,23 @@ const char* kernel_name(const pcg::PlanHost& h, uint32_t scl_lp = 0)
     return h.fixed ? sclc[i] : sclls[i];
 }
 
-// Grow the plan's scratch to `units` waves, in stream order (no device-wide sync).
-int grow_scratch(pcg_plan* p, uint64_t units, size_t elem, hipStream_t s)
+// Grow the plan's scratch to `units` waves of `per` elements each (default: the plan's
+// per-wave scratch), in stream order (no device-wide sync).
+int grow_scratch(pcg_plan* p, uint64_t units, size_t elem, hipStream_t s, uint64_t per = 0)
 {
-    if (p->scratch_floats == 0 || units <= p->scratch_frames)
+    const uint64_t need = units * (per ? per : p->scratch_floats);
+    if (need == 0 || need <= p->scratch_cap)
         return PCG_OK;
     if (p->d_scratch)
         (void)hipFreeAsync(p->d_scratch, s);
     p->d_scratch = nullptr;
-    p->scratch_frames = 0;
+    p->scratch_cap = 0;
     void* ptr = nullptr;
-    hipError_t e = hipMallocAsync(&ptr, units * p->scratch_floats * elem, s);
+    hipError_t e = hipMallocAsync(&ptr, need * elem, s);
     if (e != hipSuccess)
         return hip_fail(e, "hipMallocAsync(scratch)");
     p->d_scratch = static_cast<float*>(ptr);
-    p->scratch_frames = units;
+    p->scratch_cap = need;
     return PCG_OK;
 }
 
@@ -769,7 +771,9 @@ static int decode_impl(pcg_plan* p,
                        const uint32_t* fmap,
                        const uint32_t* fcount,
                        const int8_t* llr8 = nullptr,
-                       float* soft = nullptr);
+                       float* soft = nullptr,
+                       const int32_t* pmap = nullptr,
+                       uint32_t in_stride = 0);
 
 static int decode_adaptive(pcg_plan* p, const float* llr, uint64_t F, uint8_t* info, uint8_t* ok, float* metrics,
                            void* stream, const int8_t* llr8 = nullptr)
@@ -836,7 +840,9 @@ static int decode_impl(pcg_plan* p,
                        const uint32_t* fmap,
                        const uint32_t* fcount,
                        const int8_t* llr8,
-                       float* soft)
+                       float* soft,
+                       const int32_t* pmap,
+                       uint32_t in_stride)
 {
     const auto& h = p->host;
     pcg::KernelArgs a{};
@@ -915,7 +921,12 @@ static int decode_impl(pcg_plan* p,
     } else {
         a.scl_lp = p->scl_lp;
         a.units = (uint32_t)pcg::wave_units(F, 64 / p->scl_lp, p->wave_cap);
-        if ((rc = grow_scratch(p, a.units, sizeof(float), s)) != 0)
+        if (pmap) { // punctured frames: each wave depunctures its group into its scratch
+            a.pmap = pmap;
+            a.in_stride = in_stride;
+            a.scratch_floats = p->scratch_floats + (uint64_t)(64 / p->scl_lp) * h.N;
+        }
+        if ((rc = grow_scratch(p, a.units, sizeof(float), s, a.scratch_floats)) != 0)
             return rc;
         a.scratch = p->d_scratch;
         a.queue = p->d_queue;
@@ -1182,6 +1193,14 @@ int pcg_decode_punctured_f32(pcg_plan* p,
     DeviceGuard g(p->device);
     const auto& h = p->host;
     const uint64_t kb = (h.K + 7) / 8;
+    if (h.L > 1 && !h.fixed && !p->fast) {
+        // float list plans depuncture inside the kernel (each wave its codeword group, into its
+        // scratch slab: sclls_kernel.hip ls_depuncture) -- one launch, no staging buffer
+        if (F > 0xFFFFFFFFull)
+            return fail(PCG_E_ARG, "at most 2^32 - 1 frames per call");
+        return decode_impl(p, llr, F, info, ok, metrics, stream, nullptr, nullptr, nullptr, nullptr, punc->d_src,
+                           punc->E);
+    }
     // d_dep is reused: the depuncture below runs after the plan's previous decode
     if (int rc = order_on(p, reinterpret_cast<hipStream_t>(stream)); rc != 0)
         return rc;

@@ -59,6 +59,13 @@ struct KernelArgs {
     // lane-serial SCL with lazy bit buffers (LP >= PCG_LS_DBITS_LP): D[4 .. scl_sb-1] in LDS,
     // the rest in the global slab; 0 for the per-lane codeword rows of smaller LP
     uint32_t scl_sb;
+    // lane-serial SCL on punctured frames (pcg_decode_punctured_f32): frame f's E = in_stride
+    // received LLRs start at llr + f * in_stride, and position j of its depunctured codeword is
+    // llr[pmap[j]], or +0.0 where pmap[j] < 0 (Puncturer::depuncture, puncturer.h:92-99).  Each
+    // wave depunctures its codeword group into its scratch slab (scratch_floats includes the
+    // G x N region).  null: the frames are N LLRs each.
+    const int32_t* pmap;
+    uint32_t in_stride;
 };
 
 #ifndef PCG_RTC

@@ -256,10 +256,11 @@ PCG_DEV float4 f4_f(const float4& a, const float4& b)
 {
     return make_float4(polar_f(a.x, b.x), polar_f(a.y, b.y), polar_f(a.z, b.z), polar_f(a.w, b.w));
 }
-PCG_DEV float4 f4_g(const float4& a, const float4& b, uint32_t wb)
+// G of 4 elements with their bits at positions k0 .. k0+3 of wb (k0 + 3 < 32)
+PCG_DEV float4 f4_g(const float4& a, const float4& b, uint32_t wb, uint32_t k0 = 0)
 {
-    return make_float4(polar_g(a.x, b.x, (wb & 1u) << 31), polar_g(a.y, b.y, ((wb >> 1) & 1u) << 31),
-                       polar_g(a.z, b.z, ((wb >> 2) & 1u) << 31), polar_g(a.w, b.w, ((wb >> 3) & 1u) << 31));
+    return make_float4(polar_g_bit(a.x, b.x, wb, k0), polar_g_bit(a.y, b.y, wb, k0 + 1),
+                       polar_g_bit(a.z, b.z, wb, k0 + 2), polar_g_bit(a.w, b.w, wb, k0 + 3));
 }
 
 // Channel loads.  (Measured round 2: non-temporal loads here -- frames kept out of L2 to
@@ -552,7 +553,7 @@ PCG_DEV void ls_fg(Src src, Dst dst, const DBits& lb, uint32_t s, const Share& w
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             if ((uint32_t)u < valid) {
-                const float4 r = OPC == OP_F ? f4_f(xa[u], xb[u]) : f4_g(xa[u], xb[u], wb >> (4 * u));
+                const float4 r = OPC == OP_F ? f4_f(xa[u], xb[u]) : f4_g(xa[u], xb[u], wb, 4 * u);
                 dst.st(cb + c0 + u, r);
             }
         }
@@ -660,8 +661,8 @@ PCG_DEV void ls_fgf(Src src, Dst1 d1, Dst2 d2, const DBits& lb, uint32_t s, cons
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const float4 y0 = OPC == OP_F ? f4_f(x[0][u], x[1][u]) : f4_g(x[0][u], x[1][u], wa >> (4 * u));
-            const float4 y1 = OPC == OP_F ? f4_f(x[2][u], x[3][u]) : f4_g(x[2][u], x[3][u], wb >> (4 * u));
+            const float4 y0 = OPC == OP_F ? f4_f(x[0][u], x[1][u]) : f4_g(x[0][u], x[1][u], wa, 4 * u);
+            const float4 y1 = OPC == OP_F ? f4_f(x[2][u], x[3][u]) : f4_g(x[2][u], x[3][u], wb, 4 * u);
             d1.st(cb + c0 + u, y0);
             d1.st(cb + c0 + hq2 + u, y1);
             d2.st(cb + c0 + u, f4_f(y0, y1));
@@ -787,18 +788,18 @@ PCG_DEV void ls_fgf_root(const Ls<LP>& c, GlSt d1, Dst2 d2, const DBits& lb, con
                     x[k] = f4_f(yv[k], yv[k + 4]);
                 } else {
                     const uint32_t a = c2 + ((k & 1) ? hq : 0u) + ((k & 2) ? hq2 : 0u);
-                    x[k] = f4_g(yv[k], yv[k + 4], grp ? rw[k] >> gs : rb.at(4u * a));
+                    x[k] = (grp ? f4_g(yv[k], yv[k + 4], rw[k], gs) : f4_g(yv[k], yv[k + 4], rb.at(4u * a)));
                 }
             }
             uint32_t wa = 0, wb = 0;
             if (OPC == OP_G) {
                 const uint32_t ia = 4u * c2, ib = ia + 4u * hq2;
-                wa = grp ? lw[0] >> gs : lb.at(ia);
-                wb = grp ? lw[1] >> gs : lb.at(ib);
+                wa = grp ? lw[0] : lb.at(ia); // (grp: bit gs + j of the word, else bit j)
+                wb = grp ? lw[1] : lb.at(ib);
             }
             // x[1] = alpha[s] chunk c2+hq pairs with x[0]; x[2], x[3] = chunks c2+hq2, c2+hq2+hq
-            const float4 y0 = OPC == OP_F ? f4_f(x[0], x[1]) : f4_g(x[0], x[1], wa);
-            const float4 y1 = OPC == OP_F ? f4_f(x[2], x[3]) : f4_g(x[2], x[3], wb);
+            const float4 y0 = OPC == OP_F ? f4_f(x[0], x[1]) : f4_g(x[0], x[1], wa, grp ? gs : 0u);
+            const float4 y1 = OPC == OP_F ? f4_f(x[2], x[3]) : f4_g(x[2], x[3], wb, grp ? gs : 0u);
             d1.st(c2, y0);
             d1.st(c2 + hq2, y1);
             d2.st(c2, f4_f(y0, y1));
@@ -920,14 +921,14 @@ PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, co
                 for (int l = 1; l <= V; ++l)
 #pragma unroll
                     for (uint32_t i = 0; i < (J >> l); ++i)
-                        v[i] = ((RM >> (l - 1)) & 1) ? f4_g(v[2 * i], v[2 * i + 1], bw[k][J - (J >> (l - 1)) + i] >> gs)
+                        v[i] = ((RM >> (l - 1)) & 1) ? f4_g(v[2 * i], v[2 * i + 1], bw[k][J - (J >> (l - 1)) + i], gs)
                                                      : f4_f(v[2 * i], v[2 * i + 1]);
                 x[k] = v[0];
             }
-            const float4 y0 = OPC == OP_F ? f4_f(x[0], x[1]) : f4_g(x[0], x[1], lw[0] >> gs);
+            const float4 y0 = OPC == OP_F ? f4_f(x[0], x[1]) : f4_g(x[0], x[1], lw[0], gs);
             d1.st(c2, y0);
             if constexpr (FU) {
-                const float4 y1 = OPC == OP_F ? f4_f(x[2], x[3]) : f4_g(x[2], x[3], lw[1] >> gs);
+                const float4 y1 = OPC == OP_F ? f4_f(x[2], x[3]) : f4_g(x[2], x[3], lw[1], gs);
                 d1.st(c2 + hq2, y1);
                 d2.st(c2, f4_f(y0, y1));
             }
@@ -2044,8 +2045,8 @@ PCG_DEV void st8_child4(Ls<LP>& c, LsSt8& st, uint32_t d, uint32_t boff)
     } else { // ShortRateRNode(4): F, left(2), G, right(2), CombineBitsShort
         float a2[4] = { polar_f(st.a4[0], st.a4[2]), polar_f(st.a4[1], st.a4[3]), 0.0f, 0.0f };
         st8_child2(c, st, (d >> 3) & 3u, a2, boff);
-        a2[0] = polar_g(st.a4[0], st.a4[2], ((st.bits >> boff) & 1u) << 31);
-        a2[1] = polar_g(st.a4[1], st.a4[3], ((st.bits >> (boff + 1)) & 1u) << 31);
+        a2[0] = polar_g_bit(st.a4[0], st.a4[2], st.bits, boff);
+        a2[1] = polar_g_bit(st.a4[1], st.a4[3], st.bits, boff + 1);
         st8_child2(c, st, (d >> 5) & 3u, a2, boff + 2);
         st.bits ^= ((st.bits >> (boff + 2)) & 3u) << boff;
     }
@@ -2071,7 +2072,7 @@ PCG_DEV void ls_st8(Ls<LP>& c, Src src, uint32_t desc, uint32_t o, uint32_t& P)
     st8_child4(c, st, desc & 0xffu, 0);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-        st.a4[i] = polar_g(st.x8[i], st.x8[i + 4], ((st.bits >> i) & 1u) << 31);
+        st.a4[i] = polar_g_bit(st.x8[i], st.x8[i + 4], st.bits, (uint32_t)i);
     st8_child4(c, st, (desc >> 8) & 0xffu, 4);
     st.bits ^= (st.bits >> 4) & 0xFu; // CombineBitsShort(4)
     // the 8 bits into D[4] or the row; after branching, first take the state (slot tables,
@@ -2114,6 +2115,42 @@ PCG_DEV uint32_t crc_syn(const DBits& cw, const uint32_t* rows, uint32_t W, uint
     for (int r = 0; r < CB; ++r)
         syn ^= (acc[r] & 1u) << r;
     return syn;
+}
+
+// ---- punctured frames ------------------------------------------------------------------
+// Scratch floats of one wave without the channel region (alpha slab, tie list, D region);
+// punctured launches append the wave's G depunctured frames (G x N floats) after them.
+constexpr __host__ __device__ inline uint64_t ls_scratch_floats(uint32_t top, uint32_t mt, uint32_t Sl, uint32_t Sb)
+{
+    return ls_gl_alpha_floats(mt, Sl) + 1024ull + 64ull * ls_dgl_words(top, Sb);
+}
+// pcg_decode_punctured_f32 on a list plan: the wave's G received frames (E LLRs each) are
+// depunctured into its scratch slab -- position j = llr[pmap[j]] or +0.0 (puncturer.h:92-99:
+// fill with zeros, then scatter, here as a gather over the output) -- and every channel read of
+// the walk (c.y, the staged root-child DMA included) uses that copy: no separate depuncture pass
+// and no F x N staging buffer in HBM.  (Invalid slots of a partial group copy the last frame.)
+template <int LP>
+PCG_DEV void ls_depuncture(Ls<LP>& c, const KernelArgs& a, uint64_t frame)
+{
+    constexpr uint32_t G = 64 / LP;
+    float* ch = c.gs + ls_scratch_floats(c.top, c.mt, c.Sl, c.Sb);
+    const uint32_t q = c.N >> 2; // float4 per frame
+    for (uint32_t g = 0; g < G; ++g) {
+        const uint32_t lo = shfl((uint32_t)frame, (int)(g * LP)), hi = shfl((uint32_t)(frame >> 32), (int)(g * LP));
+        const float* row = a.llr + ((((uint64_t)hi << 32) | lo) * a.in_stride);
+#pragma unroll 2
+        for (uint32_t t = c.lane; t < q; t += 64) {
+            const int4 s = *reinterpret_cast<const int4*>(a.pmap + 4u * t);
+            float4 v;
+            v.x = s.x >= 0 ? row[s.x] : 0.0f;
+            v.y = s.y >= 0 ? row[s.y] : 0.0f;
+            v.z = s.z >= 0 ? row[s.z] : 0.0f;
+            v.w = s.w >= 0 ? row[s.w] : 0.0f;
+            *reinterpret_cast<float4*>(ch + g * c.N + 4u * t) = v;
+        }
+    }
+    wsync();
+    c.y = ch + (c.lane / LP) * c.N;
 }
 
 // ---- the kernel ------------------------------------------------------------------------
@@ -2227,6 +2264,8 @@ PCG_DEV void sclls_body(const KernelArgs& a)
         const uint64_t fs = fvalid ? slot : Fn - 1;
         const uint64_t frame = a.fmap ? (uint64_t)a.fmap[fs] : fs;
         c.y = a.llr + frame * a.N;
+        if (a.pmap) // punctured frames: depunctured into the wave's scratch first
+            ls_depuncture<LP>(c, a, frame);
         // path 0 starts at 0 (a freshly constructed decoder) or, for a reused decoder
         // instance, at the previous frame's final path-0 metric
         c.m = a.metric0;
@@ -2509,7 +2548,7 @@ int sclls_layout(uint32_t N, uint32_t L, uint32_t lp, uint32_t vleaf, uint32_t* 
         return -4;
     *wave_lds_floats = ly.total;
     *lds_stage_limit = Sl;
-    *scratch_floats = ls_gl_alpha_floats(mt, Sl) + 1024 + 64ull * ls_dgl_words(top, Sb);
+    *scratch_floats = ls_scratch_floats(top, mt, Sl, Sb);
     *virt = vt;
     *v3 = w3;
     *sb = Sb;

@@ -45,10 +45,11 @@ PCG_DEV float4 q_f(const float4& a, const float4& b)
 {
     return make_float4(polar_f(a.x, b.x), polar_f(a.y, b.y), polar_f(a.z, b.z), polar_f(a.w, b.w));
 }
-PCG_DEV float4 q_g(const float4& a, const float4& b, uint32_t nib)
+// G of 4 elements with their bits at positions k0 .. k0+3 of nib (k0 + 3 < 32)
+PCG_DEV float4 q_g(const float4& a, const float4& b, uint32_t nib, uint32_t k0 = 0)
 {
-    return make_float4(polar_g(a.x, b.x, (nib & 1u) << 31), polar_g(a.y, b.y, ((nib >> 1) & 1u) << 31),
-                       polar_g(a.z, b.z, ((nib >> 2) & 1u) << 31), polar_g(a.w, b.w, ((nib >> 3) & 1u) << 31));
+    return make_float4(polar_g_bit(a.x, b.x, nib, k0), polar_g_bit(a.y, b.y, nib, k0 + 1),
+                       polar_g_bit(a.z, b.z, nib, k0 + 2), polar_g_bit(a.w, b.w, nib, k0 + 3));
 }
 PCG_DEV float4 q_add(const float4& a, const float4& b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
 PCG_DEV uint32_t q_sgn4(const float4& v)
@@ -127,7 +128,7 @@ struct VSrc {
             return q_f(a, b);
         if (mode == 3)
             return q_add(a, b);
-        return q_g(a, b, (row[c >> 3] >> ((4u * c) & 31u)) & 0xfu);
+        return q_g(a, b, row[c >> 3], (4u * c) & 31u);
     }
     PCG_DEV float at(uint32_t i) const
     {
@@ -136,7 +137,7 @@ struct VSrc {
             return polar_f(a, b);
         if (mode == 3)
             return a + b;
-        return polar_g(a, b, ((row[i >> 5] >> (i & 31u)) & 1u) << 31);
+        return polar_g_bit(a, b, row[i >> 5], i & 31u);
     }
 };
 
@@ -939,7 +940,7 @@ PCG_DEV void q16_core(const Cw<Q>& w, const float (&a)[8], const float (&b)[8], 
     float r[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
-        r[i] = polar_g(a[i], b[i], ((bl >> i) & 1u) << 31);
+        r[i] = polar_g_bit(a[i], b[i], bl, (uint32_t)i);
     uint32_t br;
     if (!rone) {
         br = leaf8_bits((desc >> 8) & 0xffu, r);
@@ -980,7 +981,7 @@ PCG_DEV void q16x(const Cw<Q>& w, uint32_t code, uint32_t o, uint32_t desc)
 #pragma unroll
     for (uint32_t i = 0; i < 16; ++i) {
         const float p0 = q_at(v[i >> 2], i & 3u), p1 = q_at(v[4 + (i >> 2)], i & 3u);
-        x[i] = right ? polar_g(p0, p1, ((lb >> i) & 1u) << 31) : polar_f(p0, p1);
+        x[i] = right ? polar_g_bit(p0, p1, lb, i) : polar_f(p0, p1);
     }
     if ((desc >> 17) & 1u) { // the child is a size-16 leaf (code in the low byte)
         w.put(o, 16, leaf16_bits(desc & 0xffu, x));
@@ -1029,7 +1030,7 @@ PCG_DEV void q16_par(const Cw<Q>& w, uint32_t code, uint32_t o, uint32_t desc)
     float l[8];
     gbc_allf<Q, 8>(lf, base, l);
     const uint32_t bl = leaf8_bits(desc & 0xffu, l);
-    const float rg = polar_g(x, xu, ((bl >> (i & 7u)) & 1u) << 31);
+    const float rg = polar_g_bit(x, xu, bl, i & 7u);
     uint32_t br;
     if (!rone) {
         float r[8];
@@ -1061,7 +1062,7 @@ PCG_DEV void inner_body(const Cw<Q>& w, const SRC& src, uint32_t code, uint32_t 
         if (code == OP_RONE) {
             uint32_t lb = w.row[o >> 5] >> (o & 31u), l = 0, r = 0;
             for (uint32_t i = 0; i < h; ++i) {
-                const float g = polar_g(src.at(i), src.at(i + h), ((lb >> i) & 1u) << 31);
+                const float g = polar_g_bit(src.at(i), src.at(i + h), lb, i);
                 const uint32_t rs = fbits(g) >> 31;
                 l |= (((lb >> i) & 1u) ^ rs) << i;
                 r |= rs << i;
@@ -1073,7 +1074,7 @@ PCG_DEV void inner_body(const Cw<Q>& w, const SRC& src, uint32_t code, uint32_t 
         const uint32_t lb = code == OP_G ? (w.row[o >> 5] >> (o & 31u)) : 0u;
         for (uint32_t i = 0; i < h; ++i) {
             const float a = src.at(i), b = src.at(i + h);
-            dst[i] = code == OP_F ? polar_f(a, b) : (code == OP_G ? polar_g(a, b, ((lb >> i) & 1u) << 31) : a + b);
+            dst[i] = code == OP_F ? polar_f(a, b) : (code == OP_G ? polar_g_bit(a, b, lb, i) : a + b);
         }
         return;
     }

@@ -39,12 +39,21 @@ PCG_DEV float minps(float a, float b) { return a < b ? a : b; }
 PCG_DEV float maxps(float a, float b) { return a > b ? a : b; }
 
 // f: sign(a)^sign(b) | min(|a|,|b|)          avx_float.h:55-63
+// (float |.| so the compare and the select take abs source modifiers: v_cmp_lt |a|,|b|;
+// v_cndmask |b|,|a|; v_xor; v_and_or -- MINPS semantics, the second operand on ties and NaN)
 PCG_DEV float polar_f(float a, float b)
 {
-    return ubits(((fbits(a) ^ fbits(b)) & 0x80000000u) | fbits(minps(fabs_(a), fabs_(b))));
+    const float aa = __builtin_fabsf(a), ab = __builtin_fabsf(b);
+    return ubits(((fbits(a) ^ fbits(b)) & 0x80000000u) | fbits(aa < ab ? aa : ab));
 }
 // g: (a ^ signbit) + b                       avx_float.h:71-81
 PCG_DEV float polar_g(float a, float b, uint32_t signbit) { return fxor(a, signbit) + b; }
+// g with the sign flip = bit k (< 32) of w: the bit shifted to the sign position and applied
+// with one v_bitop3 (a ^ (t & 0x80000000); truth table 0x78 = S0 ^ (S1 & S2))
+PCG_DEV float polar_g_bit(float a, float b, uint32_t w, uint32_t k)
+{
+    return ubits(__builtin_amdgcn_bitop3_b32(fbits(a), w << (31u - k), 0x80000000u, 0x78)) + b;
+}
 
 template <typename T>
 PCG_DEV T shfl(T v, int src)

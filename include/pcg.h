@@ -310,10 +310,12 @@ int pcg_puncture_packed(const pcg_puncturer* punc, const uint8_t* in, uint64_t F
 
 void pcg_puncturer_destroy(pcg_puncturer* punc);
 
-/* Decode F punctured frames: llr is F x E (device), depunctured on the device into the
- * plan's staging buffer and decoded with `plan` (whose N must equal the puncturer's
- * parent length).  Outputs as pcg_decode_f32.  Stream-ordered; the staging buffer is
- * reused across calls on the same plan (ordered after the plan's previous decode). */
+/* Decode F punctured frames: llr is F x E (device), depunctured on the device and decoded
+ * with `plan` (whose N must equal the puncturer's parent length).  Outputs as
+ * pcg_decode_f32.  Float list plans depuncture inside the decode kernel (each wave its
+ * codeword group, into its scratch: one launch, no staging buffer); the other plans
+ * depuncture into a plan staging buffer first (reused across calls, ordered after the
+ * plan's previous decode).  Stream-ordered. */
 int pcg_decode_punctured_f32(pcg_plan* plan,
                              const pcg_puncturer* punc,
                              const float* llr,

@@ -181,3 +181,35 @@ def test_device_frame_source_round_trip(oracle):
     z = (a * sigma * sigma / 2.0 - s) / sigma
     assert abs(z.mean()) < 5e-3 and abs(z.std() - 1.0) < 5e-3
     assert abs((z ** 4).mean() - 3.0) < 0.05  # Gaussian kurtosis
+
+
+@pytest.mark.parametrize("E,N,K,L", [(896, 1024, 512, 8), (600, 1024, 300, 4), (1000, 1024, 512, 16),
+                                     (200, 256, 100, 2), (40, 64, 16, 32)])
+def test_fused_depuncture_list_decode(oracle, E, N, K, L):
+    """Float list plans depuncture inside the decode kernel (each wave its codeword group,
+    into its scratch: sclls_kernel.hip ls_depuncture): BB frozen sets punctured at their
+    first N - E positions (irregular gathers), tie-heavy and AWGN-like LLRs, a batch that
+    leaves the last codeword group partial -- info, ok and ordered path metrics against the
+    oracle on the oracle's own depunctured frames, on both kernels."""
+    import torch
+    from antpolarcodes_amd._native import Puncturer
+    from helpers import gpu_plan, llr_kinds
+    rng = np.random.default_rng(E + L)
+    fr = oracle.frozen_bits_bb(N, K, 0.0)
+    F = 1001
+    llr = np.concatenate([llr_kinds(rng, F // 2, E, "normal"), llr_kinds(rng, F - F // 2, E, "ints")])
+    dep = oracle.depuncture(E, fr, llr)
+    oi, ook, om, _, _ = oracle.scl_decode(N, L, fr, dep, crc=8, paths=True)
+    punc = Puncturer(E, fr, device=0)
+    for kernel in ("interp", "rtc"):
+        if kernel == "rtc" and (N, L) != (1024, 8):
+            continue  # (the shipped cache holds config 4's code; others would compile here)
+        plan = gpu_plan(N, L, fr, kernel, crc=8)
+        d_info = torch.empty((F, plan.kb), dtype=torch.uint8, device="cuda:0")
+        d_ok = torch.empty(F, dtype=torch.uint8, device="cuda:0")
+        d_met = torch.empty((F, L), dtype=torch.float32, device="cuda:0")
+        plan.decode_punctured_device(punc, _t(llr), d_info, d_ok, d_met)
+        torch.cuda.synchronize()
+        assert np.array_equal(d_info.cpu().numpy(), oi), kernel
+        assert np.array_equal(d_ok.cpu().numpy(), ook), kernel
+        assert np.array_equal(d_met.cpu().numpy().view(np.uint32), om.view(np.uint32)), kernel
