@@ -79,6 +79,7 @@ struct pcg_plan {
     std::string rtc_err;
     hipModule_t rtc_mod = nullptr;
     hipFunction_t rtc_fn = nullptr;
+    hipFunction_t rtc_fn_i8 = nullptr; // 8-bit plans: the kernel for int8 channel LLRs (rtc_fn: float LLRs)
 };
 
 namespace {
@@ -156,6 +157,7 @@ void free_plan_device(pcg_plan* p)
         (void)hipModuleUnload(p->rtc_mod);
     p->rtc_mod = nullptr;
     p->rtc_fn = nullptr;
+    p->rtc_fn_i8 = nullptr;
 }
 
 // Batches from this size on specialise a Fast-SSC plan's kernel at their first decode (the
@@ -170,13 +172,23 @@ constexpr uint64_t RTC_AUTO_FRAMES = 8192;
 // an adaptive plan's list stage (a few frames per launch); never with the op profiler.
 bool rtc_capable(const pcg_plan* p)
 {
-    if (p->host.fixed || p->dev_opprof)
+    if (p->dev_opprof)
         return false;
-    return p->host.L == 1 ? p->host.sc_kind == 2 : (p->rtc_scl && !p->walk_latency);
+    if (p->host.fixed) // the 8-bit lane-serial Fast-SSC kernel (sccs)
+        return p->host.L == 1 && p->host.sc_kind == 0;
+    return p->host.L == 1 ? p->host.sc_kind == 2 : p->rtc_scl;
+}
+
+// the specialised kernel's name (float-LLR kernel of an 8-bit plan: + "_f32")
+const char* rtc_kernel_name(const pcg_plan* p)
+{
+    return p->host.fixed ? "sccs_rtc_kernel" : (p->host.L == 1 ? "scq_rtc_kernel" : "scl_rtc_kernel");
 }
 
 std::string rtc_source(const pcg_plan* p)
 {
+    if (p->host.fixed)
+        return pcg::sccs_rtc_source(p->host, p->lds_stage_limit);
     if (p->host.L == 1)
         return pcg::scq_rtc_source(p->host);
     return pcg::scl_rtc_source(p->host, p->scl_lp, p->lds_stage_limit, p->scl_virt, p->scl_v3, p->scl_sb,
@@ -196,7 +208,7 @@ int rtc_load(pcg_plan* p)
         p->rtc_err = "plan specialisation: " + err;
         return fail(PCG_E_HIP, p->rtc_err);
     }
-    const char* fn = p->host.L == 1 ? "scq_rtc_kernel" : "scl_rtc_kernel";
+    const char* fn = rtc_kernel_name(p);
     if (p->device < 0) { // host-only plan: the source compiles; nothing to load
         p->rtc_state = 0;
         p->kernel = fn;
@@ -213,13 +225,32 @@ int rtc_load(pcg_plan* p)
         }
     }
     hipError_t e = hipModuleLoadData(&p->rtc_mod, code.data());
-    if (e == hipSuccess)
+    if (e == hipSuccess && p->host.fixed) {
+        e = hipModuleGetFunction(&p->rtc_fn_i8, p->rtc_mod, fn);
+        if (e == hipSuccess)
+            e = hipModuleGetFunction(&p->rtc_fn, p->rtc_mod, (std::string(fn) + "_f32").c_str());
+        // the specialised kernel's own occupancy (the grid-stride assignment is static)
+        int n = 0, cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->device);
+        if (e == hipSuccess &&
+            hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, p->rtc_fn_i8, 64, p->wave_lds_floats * 4u) ==
+                hipSuccess &&
+            n > 0)
+            p->wave_cap_i8 = (uint64_t)cus * (uint64_t)std::min(n, 16);
+        if (e == hipSuccess &&
+            hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&n, p->rtc_fn, 64, p->wave_lds_floats * 4u) ==
+                hipSuccess &&
+            n > 0)
+            p->wave_cap = (uint64_t)cus * (uint64_t)std::min(n, 16);
+    } else if (e == hipSuccess) {
         e = hipModuleGetFunction(&p->rtc_fn, p->rtc_mod, fn);
+    }
     if (e != hipSuccess) {
         if (p->rtc_mod)
             (void)hipModuleUnload(p->rtc_mod);
         p->rtc_mod = nullptr;
         p->rtc_fn = nullptr;
+        p->rtc_fn_i8 = nullptr;
         p->rtc_state = -1;
         p->rtc_err = std::string("plan specialisation: module load: ") + hipGetErrorString(e);
         return fail(PCG_E_HIP, p->rtc_err);
@@ -384,11 +415,12 @@ int pcg_dev_rtc_cache_name(const pcg_plan* p, char* out, size_t n)
 {
     if (!p || !out || n == 0)
         return fail(PCG_E_ARG, "null argument");
-    if (p->fast)
-        p = p->fast;
-    if (!rtc_capable(p))
+    std::string name;
+    for (const pcg_plan* q : {(const pcg_plan*)p->fast, p}) // an adaptive plan: both stages' files
+        if (q && rtc_capable(q))
+            name += (name.empty() ? "" : " ") + pcg::rtc_cache_name(rtc_source(q));
+    if (name.empty())
         return fail(PCG_E_UNSUPPORTED, "no plan-specialised kernel for this plan");
-    const std::string name = pcg::rtc_cache_name(rtc_source(p));
     snprintf(out, n, "%s", name.c_str());
     return PCG_OK;
 }
@@ -735,8 +767,17 @@ int pcg_plan_describe(const pcg_plan* p, pcg_plan_desc* d)
                           : (p->host.L == 1 && p->host.sc_kind == 2 ? p->host.scq_q : 0);
     d->dev_overrides = p->dev_overrides | (p->fast ? p->fast->dev_overrides : 0u);
     d->recomputed_stages = p->host.L > 1 && !p->host.fixed ? p->scl_virt : 0u;
-    // (an adaptive plan: its Fast-SSC stage, which pcg_plan_specialize specialises)
-    d->specialized = (p->fast ? p->fast->rtc_state : p->rtc_state) == 1 ? 1u : 0u;
+    // every stage that has a specialised kernel runs it (an adaptive plan: both stages; the
+    // 8-bit one: its Fast-SSC stage, the 8-bit list stage has none)
+    {
+        bool any = false, all = true;
+        for (const pcg_plan* q : {(const pcg_plan*)p->fast, p})
+            if (q && rtc_capable(q)) {
+                any = any || q->rtc_state == 1;
+                all = all && q->rtc_state == 1;
+            }
+        d->specialized = any && all ? 1u : 0u;
+    }
     return PCG_OK;
 }
 
@@ -744,11 +785,15 @@ static int plan_specialize(pcg_plan* p, bool wait)
 {
     if (!p)
         return fail(PCG_E_ARG, "null plan");
-    if (p->fast) // adaptive plans: their Fast-SSC stage
-        p = p->fast;
+    if (p->fast) { // adaptive plans: both stages (the list stage: float plans only)
+        const int rc = plan_specialize(p->fast, wait);
+        if (rc != 0 || !rtc_capable(p))
+            return rc;
+    }
     if (!rtc_capable(p))
-        return fail(PCG_E_UNSUPPORTED, "no plan-specialised kernel for this plan (float Fast-SSC and list "
-                                       "plans; not the 8-bit decoders, not with PCG_OPPROF)");
+        return fail(PCG_E_UNSUPPORTED, "no plan-specialised kernel for this plan (float Fast-SSC, float list "
+                                       "and 8-bit Fast-SSC plans; not the 8-bit list decoder, not with "
+                                       "PCG_OPPROF)");
     if (p->device < 0)
         return specialize(p, wait);
     DeviceGuard g(p->device);
@@ -891,11 +936,12 @@ static int decode_impl(pcg_plan* p,
         a.wave_lds_floats = pcg::sc_wave_lds_floats(h.N);
         rc = pcg::launch_sc(a, s);
     } else if (h.fixed && h.L == 1 && h.sc_kind == 0) {
+        auto_specialize(p, F); // (before the grid: a loaded kernel brings its own occupancy)
         a.units = (uint32_t)pcg::wave_units(F, 64, i8 ? p->wave_cap_i8 : p->wave_cap);
         if ((rc = grow_scratch(p, a.units, sizeof(uint32_t), s)) != 0)
             return rc;
         a.scratch = p->d_scratch;
-        rc = pcg::launch_sccs(a, s);
+        rc = p->rtc_state == 1 ? pcg::rtc_launch(i8 ? p->rtc_fn_i8 : p->rtc_fn, a, s) : pcg::launch_sccs(a, s);
     } else if (h.fixed && h.L == 1) {
         rc = pcg::launch_sc_char(a, s);
     } else if (h.fixed) {

@@ -340,6 +340,21 @@ std::string scq_rtc_source(const PlanHost& h)
     return s;
 }
 
+std::string sccs_rtc_source(const PlanHost& h, uint32_t Sl)
+{
+    std::string s = "#define PCG_RTC 1\n";
+    auto def = [&](const char* k, uint32_t v) { s += std::string("#define PCG_RTC_") + k + " " + std::to_string(v) + "u\n"; };
+    def("N", h.N);
+    def("LOG2N", h.log2N);
+    def("K", h.K);
+    def("CRC", (uint32_t)h.crc_kind);
+    s += "#define PCG_RTC_SYS " + std::to_string(h.systematic ? 1 : 0) + "\n";
+    def("SL", Sl);
+    def("NOPS", (uint32_t)h.ops.size()); // (the schedule itself stays in the plan's device buffer)
+    s += "#include \"sccs_kernel.hip\"\n";
+    return s;
+}
+
 std::string scl_rtc_source(const PlanHost& h, uint32_t lp, uint32_t Sl, uint32_t virt, uint32_t v3, uint32_t sb,
                            uint32_t fuse)
 {

@@ -16,6 +16,10 @@ namespace pcg {
 std::string scq_rtc_source(const PlanHost& h);
 std::string scl_rtc_source(const PlanHost& h, uint32_t lp, uint32_t Sl, uint32_t virt, uint32_t v3, uint32_t sb,
                            uint32_t fuse);
+// The 8-bit lane-serial Fast-SSC kernel (sccs_kernel.hip) with the plan's constants and layout
+// as literals (kernels sccs_rtc_kernel: int8 LLRs, sccs_rtc_kernel_f32: float LLRs quantised in
+// the kernel).
+std::string sccs_rtc_source(const PlanHost& h, uint32_t Sl);
 // sclls_kernel.hip (host part): "#define PCG_LS_... <value>" lines of that translation unit's
 // compile-time knobs; *nondefault = a knob differs from the source's default (a dev build)
 std::string sclls_rtc_defines(bool* nondefault);

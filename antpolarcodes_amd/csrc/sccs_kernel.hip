@@ -13,8 +13,10 @@
 #include "plan.hpp"
 #include "wave.hpp"
 
+#ifndef PCG_RTC
 #include <stdio.h>
 #include <stdlib.h>
+#endif
 
 namespace pcg {
 
@@ -396,8 +398,25 @@ PCG_DEV void bits_op(CLane<I8>& w, uint32_t code, uint32_t s, uint32_t o)
     }
 }
 
+// One schedule word: a leaf, a Combine / Copy of the bits, or an inner F / G / G0 / ROne.
 template <bool I8>
-__global__ void __launch_bounds__(64) sccs_kernel(KernelArgs a, uint32_t Sl)
+PCG_DEV void sccs_op(CLane<I8>& w, uint32_t op)
+{
+    const uint32_t code = op_code(op), s = op_stage(op), o = op_off(op);
+    if (code >= OP_C_R0)
+        w.with_src(s, [&](const auto& src) { leaf(w, code, src, 1u << s, o); });
+    else if (code == OP_COMB || code == OP_COPY0)
+        bits_op(w, code, s, o);
+    else
+        inner(w, code, s, o);
+}
+
+// (Plan-specialised kernels keep this schedule loop: the walk unrolled at compile time like
+// scq_rtc_kernel's did not finish compiling within 25 minutes for N = 1024 -- each of the 177
+// ops inlines its byte loops.  What a specialised plan folds is N, the layout, K, the detector
+// and systematic-ness: every stage-storage test against Sl / top and every loop bound over N.)
+template <bool I8>
+PCG_DEV void sccs_body(const KernelArgs& a, uint32_t Sl)
 {
     extern __shared__ uint32_t smem_c[];
     CLane<I8> w;
@@ -418,17 +437,8 @@ __global__ void __launch_bounds__(64) sccs_kernel(KernelArgs a, uint32_t Sl)
         else
             w.chan = a.llr + fr * a.N;
         w.root = 0;
-        for (uint32_t k = 0; k < a.nops; ++k) {
-            const uint32_t op = ld_const(a.ops, k);
-            const uint32_t code = op_code(op), s = op_stage(op), o = op_off(op);
-            if (code >= OP_C_R0) {
-                w.with_src(s, [&](const auto& src) { leaf(w, code, src, 1u << s, o); });
-            } else if (code == OP_COMB || code == OP_COPY0) {
-                bits_op(w, code, s, o);
-            } else {
-                inner(w, code, s, o);
-            }
-        }
+        for (uint32_t k = 0; k < a.nops; ++k)
+            sccs_op<I8>(w, ld_const(a.ops, k));
         uint32_t* r = w.row();
         if (!a.systematic) {
             for (uint32_t q = 0; q < W; ++q)
@@ -467,6 +477,34 @@ __global__ void __launch_bounds__(64) sccs_kernel(KernelArgs a, uint32_t Sl)
                 a.ok[frame] = syn == 0 ? 1 : 0;
         }
     }
+}
+
+#ifdef PCG_RTC
+template <bool I8>
+PCG_DEV void sccs_rtc(const KernelArgs& a)
+{
+    KernelArgs b = a; // the plan's constants as literals
+    b.N = PCG_RTC_N;
+    b.log2N = PCG_RTC_LOG2N;
+    b.K = PCG_RTC_K;
+    b.kb = (PCG_RTC_K + 7u) / 8u;
+    b.crc_bits = PCG_RTC_CRC;
+    b.systematic = PCG_RTC_SYS;
+    b.nops = PCG_RTC_NOPS;
+    sccs_body<I8>(b, PCG_RTC_SL);
+}
+} // namespace
+
+// the plan-specialised 8-bit Fast-SSC decoder (the plan's constants and layout as literals):
+// int8 channel LLRs / float LLRs quantised in the kernel (CharContainer::insertLlr)
+extern "C" __global__ void __launch_bounds__(64) sccs_rtc_kernel(KernelArgs a) { sccs_rtc<true>(a); }
+extern "C" __global__ void __launch_bounds__(64) sccs_rtc_kernel_f32(KernelArgs a) { sccs_rtc<false>(a); }
+
+#else
+template <bool I8>
+__global__ void __launch_bounds__(64) sccs_kernel(KernelArgs a, uint32_t Sl)
+{
+    sccs_body<I8>(a, Sl);
 }
 
 template <bool I8>
@@ -538,5 +576,7 @@ int launch_sccs(const KernelArgs& a, hipStream_t stream)
         hipLaunchKernelGGL((sccs_kernel<false>), dim3((uint32_t)grid), dim3(64), lds, stream, a, a.lds_stage_limit);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
+
+#endif // PCG_RTC
 
 } // namespace pcg

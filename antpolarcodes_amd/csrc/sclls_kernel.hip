@@ -252,6 +252,7 @@ struct GlSt {
 // independent (it is only used before any branching), the right child
 // G(y_j, y_j+N/2, bit_j) uses the path's own left-half codeword bits, which every
 // survivor inherits unchanged.
+PCG_DEV uint32_t umax32(uint32_t a, uint32_t b) { return a > b ? a : b; }
 PCG_DEV float4 f4_f(const float4& a, const float4& b)
 {
     return make_float4(polar_f(a.x, b.x), polar_f(a.y, b.y), polar_f(a.z, b.z), polar_f(a.w, b.w));
@@ -1383,6 +1384,69 @@ PCG_DEV void weak_fast(Src src, uint32_t sl, uint32_t n, uint32_t kk, float (&T)
     }
 }
 
+// The same pass on 32-bit keys (PCG_WEAK_K32): the |llr| bits with their low log2(n) bits
+// replaced by the element index, kept by a v_min_u32 / v_max_u32 insertion chain (two ops per
+// kept entry and element instead of a compare and four selects).  The keys order the elements
+// as (value, index) does except among values that agree above those low bits; so when two of
+// the first kk+1 kept keys agree there, false is returned and the float pass runs.  The kept
+// entries' exact values are re-read (kk loads).
+#ifndef PCG_WEAK_K32
+#define PCG_WEAK_K32 1
+#endif
+template <int LP, int KEEP, typename Src>
+PCG_DEV bool weak_keys(Src src, uint32_t sl, uint32_t n, uint32_t kk, float (&T)[4], uint32_t (&I)[4],
+                       uint32_t& par)
+{
+    const uint32_t cb = (uint32_t)__builtin_ctz(n), cm = (1u << cb) - 1u;
+    uint32_t sk[KEEP];
+#pragma unroll
+    for (int j = 0; j < KEEP; ++j)
+        sk[j] = ~0u;
+    uint32_t px = 0;
+    constexpr int U = Pre<Src>::U;
+    stream<U>(src, n >> 2, sl, [&](const float4 (&x)[U], uint32_t c0, uint32_t valid) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if ((uint32_t)u < valid) {
+                const uint32_t xb[4] = { fbits(x[u].x), fbits(x[u].y), fbits(x[u].z), fbits(x[u].w) };
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    px ^= xb[e];
+                    uint32_t key = (xb[e] & 0x7fffffffu & ~cm) | (4u * (c0 + u) + e);
+#pragma unroll
+                    for (int j = 0; j < KEEP; ++j) {
+                        const uint32_t lo = key < sk[j] ? key : sk[j];
+                        key = umax32(key, sk[j]);
+                        sk[j] = lo;
+                    }
+                }
+            }
+        }
+    });
+    par = px;
+    bool near = false;
+#pragma unroll
+    for (int j = 0; j + 1 < KEEP; ++j)
+        if ((uint32_t)j < kk)
+            near = near || (sk[j] >> cb) == (sk[j + 1] >> cb);
+    if (near)
+        return false;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t i = sk[j < KEEP ? j : 0] & cm;
+        if ((uint32_t)j < kk) {
+            const float4 v = src.ld(i >> 2, sl);
+            const uint32_t e = i & 3u;
+            T[j] = fabs_(e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w);
+            I[j] = i;
+        } else {
+            T[j] = 0.0f;
+            I[j] = (uint32_t)j;
+        }
+    }
+    return true;
+}
+
 // Register version for n == 8 (and the same selection passes as ls_weak).
 PCG_DEV void weak8(const float (&v)[8], uint32_t kk, float (&T4)[4], uint32_t (&I4)[4], uint32_t& par)
 {
@@ -1655,13 +1719,224 @@ PCG_DEV uint64_t bit_pick(const uint64_t (&k)[8], uint32_t p, uint32_t gb, uint3
     return p < np ? mine : 0ull;
 }
 
+// ---- 32-bit keys (PCG_SEL_K32) ---------------------------------------------------------
+// The bitonic merge on one dword per candidate: the value's order image (+0 and -0 mapped to
+// one image) with its low CB = 3 + log2(LP) bits replaced by ~(path << 3 | j), so a compare-
+// exchange is a v_max_u32 / v_min_u32 on a DPP operand instead of a 64-bit compare and four
+// selects.  These keys order the candidates exactly as the 64-bit keys do, except among
+// candidates whose values agree above the CB low bits ("near ties", relative 2^-(23-CB): a
+// class of equal truncated values comes out contiguous, in any order).  So the first R
+// selected keys are checked pairwise: a near tie anywhere -- exact ties and +-0 included -- sends
+// the wave to the exact 64-bit sort (and from there, on a true tie, to the literal selection);
+// otherwise the order, the survivors and the tie test are the 64-bit sort's.  Measured on
+// config 3 with the selection ablated: selection is 27 % of the list kernel's VALU
+// instructions (profiles/r04e_scl8_ablation.txt).
+#ifndef PCG_SEL_K32
+#define PCG_SEL_K32 1
+#endif
+PCG_DEV uint32_t ordz(float v)
+{
+    const uint32_t o = ord_of(v);
+    return o == 0x7fffffffu ? 0x80000000u : o; // -0 -> the image of +0
+}
+PCG_DEV void cx32(uint32_t (&k)[8], int a, int b)
+{
+    const uint32_t ka = k[a], kb = k[b];
+    k[a] = umax32(ka, kb);
+    k[b] = ka > kb ? kb : ka;
+}
+template <int K>
+PCG_DEV void local_order32(uint32_t (&k)[8])
+{
+    if constexpr (K == 2)
+        cx32(k, 0, 1);
+    else if constexpr (K == 8)
+        cx32(k, 3, 4);
+}
+template <int K, int D>
+PCG_DEV void bit_lanes32(uint32_t (&k)[8], uint32_t p)
+{
+    if constexpr (D >= 1) {
+        const bool low = (p & D) == 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const uint32_t o = xpartner<D>(k[j]);
+            k[j] = low ? umax32(k[j], o) : (k[j] > o ? o : k[j]);
+        }
+        bit_lanes32<K, D / 2>(k, p);
+    }
+}
+template <int K, int D>
+PCG_DEV void bit_regs32(uint32_t (&k)[8])
+{
+    if constexpr (D >= 1) {
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            if ((j & D) == 0)
+                cx32(k, j, j | D);
+        bit_regs32<K, D / 2>(k);
+    }
+}
+template <int LP, int K, int B>
+PCG_DEV void bit_level32(uint32_t (&k)[8], uint32_t p)
+{
+    if constexpr (B < LP) {
+        const bool low = (p & B) == 0;
+        uint32_t t[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            t[j] = mirror_lane<2 * B>(k[K - 1 - j]);
+#pragma unroll
+        for (int j = 0; j < K; ++j)
+            k[j] = low ? umax32(k[j], t[j]) : (k[j] > t[j] ? t[j] : k[j]);
+        bit_lanes32<K, B / 2>(k, p);
+        bit_regs32<K, K / 2>(k);
+        bit_level32<LP, K, 2 * B>(k, p);
+    }
+}
+template <int LP>
+constexpr uint32_t k32_cb()
+{
+    return LP <= 2 ? 4u : LP <= 4 ? 5u : LP <= 8 ? 6u : LP <= 16 ? 7u : 8u;
+}
+// Selection on 32-bit keys: true and (val, src, jsel) when no group has a near tie among its
+// first R selected keys, else false (the caller runs the exact sort).
+template <int LP, int K>
+PCG_DEV bool k32_select(const Ls<LP>& c, const float (&cv)[8], uint32_t P, uint32_t np, uint32_t R, float& val,
+                        uint32_t& src, uint32_t& jsel)
+{
+    constexpr uint32_t CB = k32_cb<LP>(), cm = (1u << CB) - 1u;
+    const bool act = c.p < P;
+    uint32_t q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        q[j] = (act && j < K) ? ((ordz(cv[j]) & ~cm) | (~((c.p << 3) | (uint32_t)j) & cm)) : 0u;
+    local_order32<K>(q);
+    bit_level32<LP, K, 1>(q, c.p);
+    bool near = false;
+#pragma unroll
+    for (int j = 0; j + 1 < K; ++j)
+        if (c.p * K + j + 1 < R)
+            near = near | ((q[j] >> CB) == (q[j + 1] >> CB));
+    const uint32_t nxt = shfl(q[0], (int)(c.gb | ((c.p + 1) & (LP - 1))));
+    if (c.p + 1 < LP && c.p * K + K < R)
+        near = near | ((q[K - 1] >> CB) == (nxt >> CB));
+    if (ballot(near) != 0ull)
+        return false;
+    const int sl = (int)(c.gb | (c.p / K));
+    uint32_t mk = 0;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const uint32_t x = shfl(q[j], sl);
+        if ((uint32_t)j == c.p % K)
+            mk = x;
+    }
+    const uint32_t code = ~mk & cm;
+    src = code >> 3;
+    jsel = code & 7u;
+    // the exact value of the candidate, from its path's lane
+    float vv = 0.0f;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        const float x = shfl(cv[j], (int)(c.gb | src));
+        if ((uint32_t)j == jsel)
+            vv = x;
+    }
+    val = vv;
+    return true;
+}
+
+// ---- value merge rounds (PCG_SEL_VMERGE) ------------------------------------------------
+// The same selection on 32-bit order images of the values alone: round r takes the group
+// maximum of the lanes' heads (DPP butterflies of v_max_u32), the lowest lane holding it pops
+// its head, and slot r records (value, lane); the popped position of slot r's candidate is the
+// number of rounds its lane won before r.  Without a tie among the first R selected values
+// (equal adjacent values, or two lanes holding the maximum in one round -- then the literal
+// selection runs, as for the keyed variants) every round's maximum is unique, so the result is
+// the keyed merge's.  The lists come in locally ordered (local_order: for K = 8 positions 3 / 4,
+// for K = 2 positions 0 / 1 may have been exchanged), which maps a popped position back to the
+// candidate index.
+#ifndef PCG_SEL_VMERGE
+#define PCG_SEL_VMERGE 0
+#endif
+template <int LP>
+PCG_DEV uint32_t grp_umax(uint32_t v)
+{
+    if constexpr (LP > 1) v = umax32(v, bfly<1>(v));
+    if constexpr (LP > 2) v = umax32(v, bfly<2>(v));
+    if constexpr (LP > 4) v = umax32(v, bfly<4>(v));
+    if constexpr (LP > 8) v = umax32(v, bfly<8>(v));
+    if constexpr (LP > 16) v = umax32(v, bfly<16>(v));
+    if constexpr (LP > 32) v = umax32(v, bfly<32>(v));
+    return v;
+}
+template <int LP, int K>
+PCG_DEV void vmerge_select(const Ls<LP>& c, const uint64_t (&k)[8], uint32_t P, uint32_t np, uint32_t R, float& val,
+                           uint32_t& src, uint32_t& jsel, bool& tie)
+{
+    uint32_t hv[K];
+    uint32_t swp = 0; // the local order exchanged a pair of positions
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+        hv[j] = (uint32_t)(k[j] >> 32);
+        const uint32_t jj = ~(uint32_t)k[j] & 7u; // candidate index of position j
+        swp |= jj != (uint32_t)j ? 1u : 0u;
+    }
+    const uint64_t gmask = LP == 64 ? ~0ull : ((1ull << LP) - 1ull);
+    uint32_t won = 0, mh = 0, mw = c.p, prevh = 0;
+    bool t = false;
+    for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t h = grp_umax<LP>(hv[0]);
+        const uint64_t at = ballot(hv[0] == h);
+        const uint32_t gm = (uint32_t)((at >> c.gb) & gmask);
+        const uint32_t w = (uint32_t)__builtin_ctz(gm);
+        t = t | ((gm & (gm - 1u)) != 0u) | ((r > 0) & ord_eq(h, prevh));
+        prevh = h;
+        const bool mine = c.p == r;
+        mh = mine ? h : mh;
+        mw = mine ? w : mw;
+        const bool win = c.p == w;
+        won |= (win && r < 32u) ? 1u << r : 0u;
+#pragma unroll
+        for (int j = 0; j + 1 < K; ++j)
+            hv[j] = win ? hv[j + 1] : hv[j];
+        hv[K - 1] = win ? 0u : hv[K - 1];
+    }
+    tie = t;
+    const int sl = (int)(c.gb | mw);
+    const uint32_t wsrc = shfl(won, sl), ssrc = shfl(swp, sl);
+    uint32_t pos = (uint32_t)__builtin_popcount(wsrc & ((1u << (c.p & 31u)) - 1u));
+    if (ssrc && K == 8 && (pos == 3u || pos == 4u))
+        pos ^= 7u;
+    if (ssrc && K == 2)
+        pos ^= 1u;
+    val = val_of(mh);
+    src = mw;
+    jsel = pos;
+}
+
 template <int LP, int K>
 PCG_DEV void ls_select(const Ls<LP>& c, const float (&cv)[8], uint32_t P, uint32_t np, float& val, uint32_t& src,
                        uint32_t& jsel)
 {
     LS_T0();
+#ifdef PCG_DEV_ABL_SEL // dev ablation (wrong results, cost measurement only): no selection network
+    val = cv[0];
+    src = c.p < P ? c.p : 0u;
+    jsel = 0;
+    return;
+#endif
     const uint32_t C = P * K;
     const bool act = c.p < P;
+    const uint32_t R = C > np ? np + 1 : C;
+    if constexpr (PCG_SEL_K32 && LP <= 8) { // (LP = 32: 8 code bits leave near ties common, and the
+                                              // 32-bit network beside the exact one spills: 1.12e6 ->
+                                              // 6.7e5 cw/s on config 5, profiles/r04g_*)
+        if (k32_select<LP, K>(c, cv, P, np, R, val, src, jsel)) {
+            LS_STAMP(c, 50);
+            return;
+        }
+    }
     uint64_t k[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -1674,11 +1949,12 @@ PCG_DEV void ls_select(const Ls<LP>& c, const float (&cv)[8], uint32_t P, uint32
 #else
     local_order<K>(k);
 #endif
-    const uint32_t R = C > np ? np + 1 : C;
     float prev = 0.0f;
     bool tie = false;
     uint64_t mine = 0;
-    if constexpr (LP >= PCG_SEL_BITONIC_LP || K <= PCG_SEL_BITONIC_K) {
+    if constexpr (PCG_SEL_VMERGE >= 2 || (PCG_SEL_VMERGE == 1 && LP <= 8)) {
+        vmerge_select<LP, K>(c, k, P, np, R, val, src, jsel, tie);
+    } else if constexpr (LP >= PCG_SEL_BITONIC_LP || K <= PCG_SEL_BITONIC_K) {
         bit_level<LP, K, 1>(k, c.p);
         mine = bit_pick<LP, K>(k, c.p, c.gb, np, R, tie);
     } else
@@ -1695,10 +1971,12 @@ PCG_DEV void ls_select(const Ls<LP>& c, const float (&cv)[8], uint32_t P, uint32
             k[j] = win ? k[j + 1] : k[j];
         k[K - 1] = win ? 0ull : k[K - 1];
     }
-    val = val_of((uint32_t)(mine >> 32));
-    const uint32_t mc = ~(uint32_t)mine;
-    src = (mc >> 3) & 31u;
-    jsel = mc & 7u;
+    if constexpr (!(PCG_SEL_VMERGE >= 2 || (PCG_SEL_VMERGE == 1 && LP <= 8))) {
+        val = val_of((uint32_t)(mine >> 32));
+        const uint32_t mc = ~(uint32_t)mine;
+        src = (mc >> 3) & 31u;
+        jsel = mc & 7u;
+    }
     if (ballot(tie) == 0ull) {
         LS_STAMP(c, 50);
         return;
@@ -1793,10 +2071,22 @@ PCG_DEV void ls_branch_leaf(Ls<LP>& c, Src src, uint32_t code, uint32_t s, uint3
         const float v[8] = { a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w };
         weak8(v, kk, T, I, par);
     } else {
-        bool tie;
-        weak_fast<LP>(src, sl, n, kk, T, I, par, tie);
-        if (tie)
-            ls_weak(c, src, sl, n, kk, T, I, par);
+#ifdef PCG_DEV_ABL_WEAK // dev ablation (wrong results, cost measurement only): no weak-LLR search
+        const float4 a = src.ld(0, sl);
+        T[0] = fabs_(a.x); T[1] = fabs_(a.y); T[2] = fabs_(a.z); T[3] = fabs_(a.w);
+        I[0] = 0; I[1] = 1; I[2] = 2; I[3] = 3;
+        par = fbits(a.x);
+#else
+        bool done = false;
+        if constexpr (PCG_WEAK_K32 && LP <= 8) // (LP = 32 is at its register limit)
+            done = kk == 2u ? weak_keys<LP, 3>(src, sl, n, kk, T, I, par) : weak_keys<LP, 5>(src, sl, n, kk, T, I, par);
+        if (!done) {
+            bool tie;
+            weak_fast<LP>(src, sl, n, kk, T, I, par, tie);
+            if (tie)
+                ls_weak(c, src, sl, n, kk, T, I, par);
+        }
+#endif
     }
     LS_STAMP(c, 53);
     float cv[8];
@@ -2570,6 +2860,9 @@ std::string sclls_rtc_defines(bool* nondefault)
     d("PCG_STG_GM", PCG_STG_GM, 1);
     d("PCG_SEL_BITONIC_LP", PCG_SEL_BITONIC_LP, 16);
     d("PCG_SEL_BITONIC_K", PCG_SEL_BITONIC_K, 4);
+    d("PCG_SEL_VMERGE", PCG_SEL_VMERGE, 0);
+    d("PCG_SEL_K32", PCG_SEL_K32, 1);
+    d("PCG_WEAK_K32", PCG_WEAK_K32, 1);
     d("PCG_LS_MINW", PCG_LS_MINW, 2);
 #ifdef PCG_LS_FULL_LOCAL_SORT
     s += "#define PCG_LS_FULL_LOCAL_SORT 1\n";

@@ -22,10 +22,12 @@ CACHE = os.path.join(HERE, "lib", "rtc")
 def bench_codes():
     """(N, L, frozen spec, crc, systematic): the configurations bench.py decodes."""
     return [
-        (1024, 1, ("BB", 512), 8, True),     # config 2 (and the adaptive decoder's first stage)
+        (1024, 1, ("BB", 512), 8, True),     # config 2
         (1024, 8, ("BB", 512), 8, True),     # config 3
+        (1024, 8, ("BB", 512), 8, True, "adaptive"),  # config 3 with AdaptiveFloat (both stages)
         (1024, 8, ("5G", 512), 11, True),    # config 4
         (4096, 32, ("BB", 2048), 8, True),   # config 5
+        (1024, 1, ("BB", 512), 8, True, "char"),      # sc_char, and adaptive8_char's first stage
     ]
 
 
@@ -50,12 +52,19 @@ def test_codes():
         out.append((N, L, ("BB", K), crc, sysm))          # test_rtc_list_plans
     out.append((1024, 8, ("5G", 512), 0, True))           # config 4's decoder core with the Dummy detector
     out.append((1024, 1, ("5G", 512), 11, True))          # config 4 through Fast-SSC
+    for crc in (8, 16, 32):                               # test_adaptive_matches_oracle: both stages
+        out.append((1024, 8, ("BB", 512), crc, True, "adaptive"))
+    try:                                                  # test_gpu_char.py::test_scc_rtc_kernel
+        from test_gpu_char import rtc_char_codes
+        for N, fr, sysm, crc in rtc_char_codes():
+            out.append((N, 1, ("set", tuple(int(v) for v in fr)), crc, sysm, "char"))
+    except ImportError:
+        pass
     return out
 
 
 def _key(c):
-    N, L, (kind, arg), crc, sysm = c
-    return (N, L, kind, arg, crc, sysm)
+    return tuple(c[:2]) + tuple(c[2]) + tuple(c[3:])
 
 
 def codes():
@@ -69,7 +78,9 @@ def codes():
 
 def _one(c):
     """Compile one code in a child process (hiprtc state stays out of the caller)."""
-    N, L, (kind, arg), crc, sysm = c
+    N, L, (kind, arg), crc, sysm = c[:5]
+    adaptive = len(c) > 5 and c[5] == "adaptive"
+    fixed = len(c) > 5 and c[5] == "char"
     prog = (
         "import sys; sys.path.insert(0, %r)\n"
         "from antpolarcodes_amd._native import Plan, PcgError\n"
@@ -77,19 +88,19 @@ def _one(c):
         "kind, arg = %r, %r\n"
         "fr = list(arg) if kind == 'set' else frozen_bits(%d, arg, 0.0, kind)\n"
         "try:\n"
-        "    p = Plan(%d, %d, fr, systematic=%r, crc=%d, device=-1)\n"
+        "    p = Plan(%d, %d, fr, systematic=%r, crc=%d, device=-1, adaptive=%r, fixed=%r)\n"
         "except PcgError:\n"
         "    sys.exit(0)  # a frozen set the decoder rejects: nothing to compile\n"
         "p.specialize()\n"
         "import ctypes\n"
         "from antpolarcodes_amd._native import lib\n"
-        "b = ctypes.create_string_buffer(64)\n"
-        "lib().pcg_dev_rtc_cache_name(p._h, b, 64)\n"
-        "print('RTCFILE', b.value.decode())\n" % (os.path.dirname(HERE), kind, arg, N, N, L, sysm, crc))
+        "b = ctypes.create_string_buffer(128)\n"
+        "lib().pcg_dev_rtc_cache_name(p._h, b, 128)\n"
+        "print('RTCFILE', b.value.decode())\n" % (os.path.dirname(HERE), kind, arg, N, N, L, sysm, crc, adaptive, fixed))
     env = {k: v for k, v in os.environ.items() if not k.startswith("PCG_")}  # the default layouts
     env["PCG_RTC_CACHE"] = CACHE
     r = subprocess.run([sys.executable, "-c", prog], env=env, capture_output=True, text=True)
-    names = [ln.split()[1] for ln in r.stdout.splitlines() if ln.startswith("RTCFILE ")]
+    names = [n for ln in r.stdout.splitlines() if ln.startswith("RTCFILE ") for n in ln.split()[1:]]
     return c, r.returncode, r.stderr[-2000:], names
 
 

@@ -153,9 +153,10 @@ def _counter_rows(outdir):
 
 
 def specialize(plan):
-    """Plan-specialised kernel (pcg_plan_specialize: hiprtc, Fast-SSC float plans and the
-    adaptive plans' Fast-SSC stage) before the warmup, so its compile is never timed and the
-    kernel name is the one that runs.  PCG_RTC=0 keeps the interpreter kernel."""
+    """Plan-specialised kernels (pcg_plan_specialize: hiprtc, float Fast-SSC and list plans,
+    both stages of a float adaptive plan; the shipped cache holds the benchmark codes) before
+    the warmup, so a compile is never timed and the kernel name is the one that runs.
+    PCG_RTC=0 keeps the interpreter kernels."""
     from antpolarcodes_amd._native import PCG_E_UNSUPPORTED, PcgError
     if os.environ.get("PCG_RTC") == "0":
         return

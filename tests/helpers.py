@@ -75,9 +75,8 @@ def gpu_plan(N, L, frozen, kernel="interp", device=0, **kw):
     if kernel == "rtc":
         p.specialize()
         assert p.describe()["specialized"] == 1
-        if not kw.get("adaptive"):  # (an adaptive plan names its list stage's kernel)
-            want = "scq_rtc_kernel" if L == 1 else "scl_rtc_kernel"
-            assert p.kernel_name() == want, p.kernel_name()
+        want = "scq_rtc_kernel" if L == 1 else "scl_rtc_kernel"  # (adaptive: its list stage's)
+        assert p.kernel_name() == want, p.kernel_name()
     else:
         assert p.describe()["specialized"] == 0 and "rtc" not in p.kernel_name(), p.kernel_name()
     return p

@@ -226,3 +226,52 @@ def test_adaptive_char_matches_oracle(oracle, crc):
     assert np.array_equal(gi, exp) and np.array_equal(gok, eok)
     gi, gok, _ = p.decode_host(llr * 10.0)  # float frames, quantised in the kernels
     assert np.array_equal(gi, exp) and np.array_equal(gok, eok)
+
+
+# ------------------------------------------------------------------ specialised FastSscFipChar
+def rtc_char_codes():
+    """(N, frozen, systematic, crc) the specialised 8-bit Fast-SSC kernel is checked on (their
+    code objects ship with the library: antpolarcodes_amd/rtc_warm.py)."""
+    out = [(N, frozen_bits(N, max(8, N // 2), 0.0), True, 8) for N in (8, 32, 128, 256, 1024)]
+    out += [(64, fr, True, 0) for n, fr in cover_codes() if n == 64]
+    out += [(1024, frozen_bits(1024, 512, 0.0), sysm, crc) for sysm in (True, False) for crc in (0, 16, 32)]
+    return out
+
+
+def test_scc_rtc_kernel(oracle):
+    """The 8-bit Fast-SSC decoder on its plan-specialised kernel (sccs_rtc_kernel: the plan's
+    constants and layout as literals): int8 frames of every family and float frames quantised in the
+    kernel, bit-exact against the oracle, over BB codes, every 8-bit node kind at n = 64 and the
+    detector / systematic variants."""
+    from antpolarcodes_amd._native import Plan
+    rng = np.random.default_rng(77)
+    for N, fr, sysm, crc in rtc_char_codes():
+        p = Plan(N, 1, fr, systematic=sysm, crc=crc, device=0, fixed=True)
+        p.specialize()
+        assert p.kernel_name() == "sccs_rtc_kernel" and p.describe()["specialized"] == 1
+        for kind in KINDS:
+            x = i8_kinds(rng, 96, N, kind)
+            gi, gok, _ = p.decode_host_i8(x)
+            oi, ook = oracle.scc_decode(N, fr, x, sysm, crc)
+            assert np.array_equal(gi, oi) and np.array_equal(gok, ook), (N, kind, sysm, crc)
+        x = (rng.normal(0, 60, (64, N)) * 10.0 ** rng.uniform(-1, 1.5, (64, N))).astype(np.float32)
+        gi, gok, _ = p.decode_host(x)
+        oi, ook = oracle.scc_decode(N, fr, x, sysm, crc)
+        assert np.array_equal(gi, oi) and np.array_equal(gok, ook), (N, "float", sysm, crc)
+
+
+def test_scc_rtc_config_batch(oracle):
+    """sc_char's bench code (N=1024 K=512 CRC-8) on 2^16 int8 AWGN frames through the
+    specialised kernel, against the oracle and the interpreter kernel."""
+    from antpolarcodes_amd._native import Plan
+    fr = frozen_bits(1024, 512, 0.0)
+    llr, _, _ = frames.awgn_frames(1024, fr, 1 << 16, 2.0, seed=8, crc=8)
+    x = np.clip(np.rint(llr * 8.0), -128, 127).astype(np.int8)
+    p = Plan(1024, 1, fr, crc=8, device=0, fixed=True)
+    gi0, gok0, _ = p.decode_host_i8(x)
+    p.specialize()
+    assert p.kernel_name() == "sccs_rtc_kernel"
+    gi, gok, _ = p.decode_host_i8(x)
+    oi, ook = oracle.scc_decode(1024, fr, x, True, 8)
+    assert np.array_equal(gi, oi) and np.array_equal(gok, ook)
+    assert np.array_equal(gi0, oi) and np.array_equal(gok0, ook)

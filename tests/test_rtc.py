@@ -46,11 +46,17 @@ def test_specialize_compiles_list_plan(oracle):
 
 
 def test_specialize_unsupported_plans(oracle):
+    """The 8-bit list decoder has no specialised kernel; the 8-bit Fast-SSC one has (its
+    constants and layout as literals: sccs_rtc_kernel for int8 LLRs, sccs_rtc_kernel_f32 for
+    float ones)."""
     from antpolarcodes_amd._native import PcgError, PCG_E_UNSUPPORTED
-    for kw in ({"fixed": True}, {"fixed": True, "L": 8}):
-        with pytest.raises(PcgError) as e:
-            _host_plan(oracle, 256, 128, **kw).specialize()
-        assert e.value.code == PCG_E_UNSUPPORTED
+    with pytest.raises(PcgError) as e:
+        _host_plan(oracle, 256, 128, L=8, fixed=True).specialize()
+    assert e.value.code == PCG_E_UNSUPPORTED
+    p = _host_plan(oracle, 256, 128, fixed=True)
+    assert p.kernel_name() == "sccs_kernel"
+    p.specialize()
+    assert p.kernel_name() == "sccs_rtc_kernel"
 
 
 def _run(code, env_extra, timeout=600):
@@ -118,8 +124,9 @@ def test_shipped_cache_holds_the_benchmark_codes():
     """The build (antpolarcodes_amd/rtc_warm.py) ships the specialised kernels of the benchmark
     configurations next to the library: they load without any compile."""
     code = ("from antpolarcodes_amd.rtc_warm import bench_codes\n"
-            "for N, L, (kind, K), crc, sysm in bench_codes():\n"
-            "    p = Plan(N, L, frozen_bits(N, K, 0.0, kind), systematic=sysm, crc=crc, device=-1)\n"
+            "for N, L, (kind, K), crc, sysm, *ad in bench_codes():\n"
+            "    p = Plan(N, L, frozen_bits(N, K, 0.0, kind), systematic=sysm, crc=crc, device=-1,\n"
+            "             adaptive=bool(ad))\n"
             "    p.specialize()\n"
             "print('compiles', lib().pcg_dev_rtc_compiles())\n")
     assert "compiles 0" in _run(code, {"PCG_RTC_CACHE": "0"}, timeout=120)
