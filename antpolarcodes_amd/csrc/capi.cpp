@@ -174,21 +174,26 @@ bool rtc_capable(const pcg_plan* p)
 {
     if (p->dev_opprof)
         return false;
-    if (p->host.fixed) // the 8-bit lane-serial Fast-SSC kernel (sccs)
-        return p->host.L == 1 && p->host.sc_kind == 0;
+    if (p->host.fixed) // the 8-bit lane-serial kernels (sccs, scl_char)
+        return p->host.L > 1 || p->host.sc_kind == 0;
     return p->host.L == 1 ? p->host.sc_kind == 2 : p->rtc_scl;
 }
 
 // the specialised kernel's name (float-LLR kernel of an 8-bit plan: + "_f32")
 const char* rtc_kernel_name(const pcg_plan* p)
 {
-    return p->host.fixed ? "sccs_rtc_kernel" : (p->host.L == 1 ? "scq_rtc_kernel" : "scl_rtc_kernel");
+    if (p->host.fixed)
+        return p->host.L == 1 ? "sccs_rtc_kernel" : "scl_char_rtc_kernel";
+    return p->host.L == 1 ? "scq_rtc_kernel" : "scl_rtc_kernel";
 }
+
+uint32_t list_pow2(uint32_t L);
 
 std::string rtc_source(const pcg_plan* p)
 {
     if (p->host.fixed)
-        return pcg::sccs_rtc_source(p->host, p->lds_stage_limit);
+        return p->host.L == 1 ? pcg::sccs_rtc_source(p->host, p->lds_stage_limit)
+                              : pcg::sclc_rtc_source(p->host, list_pow2(p->host.L), p->lds_stage_limit);
     if (p->host.L == 1)
         return pcg::scq_rtc_source(p->host);
     return pcg::scl_rtc_source(p->host, p->scl_lp, p->lds_stage_limit, p->scl_virt, p->scl_v3, p->scl_sb,
@@ -791,9 +796,8 @@ static int plan_specialize(pcg_plan* p, bool wait)
             return rc;
     }
     if (!rtc_capable(p))
-        return fail(PCG_E_UNSUPPORTED, "no plan-specialised kernel for this plan (float Fast-SSC, float list "
-                                       "and 8-bit Fast-SSC plans; not the 8-bit list decoder, not with "
-                                       "PCG_OPPROF)");
+        return fail(PCG_E_UNSUPPORTED, "no plan-specialised kernel for this plan (not with PCG_OPPROF; the "
+                                       "8-bit Fast-SSC decoder on its one-codeword-per-wave kernel has none)");
     if (p->device < 0)
         return specialize(p, wait);
     DeviceGuard g(p->device);
@@ -945,11 +949,12 @@ static int decode_impl(pcg_plan* p,
     } else if (h.fixed && h.L == 1) {
         rc = pcg::launch_sc_char(a, s);
     } else if (h.fixed) {
+        auto_specialize(p, F); // (before the grid: a loaded kernel brings its own occupancy)
         a.units = (uint32_t)pcg::wave_units(F, 64 / list_pow2(h.L), i8 ? p->wave_cap_i8 : p->wave_cap);
         if ((rc = grow_scratch(p, a.units, sizeof(uint32_t), s)) != 0)
             return rc;
         a.scratch = p->d_scratch;
-        rc = pcg::launch_scl_char(a, s);
+        rc = p->rtc_state == 1 ? pcg::rtc_launch(i8 ? p->rtc_fn_i8 : p->rtc_fn, a, s) : pcg::launch_scl_char(a, s);
     } else if (h.L == 1 && h.sc_kind == 2) {
         a.units = (uint32_t)pcg::wave_units(F, 64 / h.scq_q, p->wave_cap);
         a.ops = p->d_ops + h.ops.size(); // the fused schedule (plan.cpp fuse_sc16)

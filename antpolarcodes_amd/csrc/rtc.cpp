@@ -355,6 +355,23 @@ std::string sccs_rtc_source(const PlanHost& h, uint32_t Sl)
     return s;
 }
 
+std::string sclc_rtc_source(const PlanHost& h, uint32_t lp, uint32_t Sl)
+{
+    std::string s = "#define PCG_RTC 1\n";
+    auto def = [&](const char* k, uint32_t v) { s += std::string("#define PCG_RTC_") + k + " " + std::to_string(v) + "u\n"; };
+    def("LP", lp);
+    def("N", h.N);
+    def("LOG2N", h.log2N);
+    def("K", h.K);
+    def("L", h.L);
+    def("CRC", (uint32_t)h.crc_kind);
+    s += "#define PCG_RTC_SYS " + std::to_string(h.systematic ? 1 : 0) + "\n";
+    def("SL", Sl);
+    def("NOPS", (uint32_t)h.ops.size());
+    s += "#include \"scl_char_kernel.hip\"\n";
+    return s;
+}
+
 std::string scl_rtc_source(const PlanHost& h, uint32_t lp, uint32_t Sl, uint32_t virt, uint32_t v3, uint32_t sb,
                            uint32_t fuse)
 {

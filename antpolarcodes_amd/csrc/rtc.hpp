@@ -20,6 +20,8 @@ std::string scl_rtc_source(const PlanHost& h, uint32_t lp, uint32_t Sl, uint32_t
 // as literals (kernels sccs_rtc_kernel: int8 LLRs, sccs_rtc_kernel_f32: float LLRs quantised in
 // the kernel).
 std::string sccs_rtc_source(const PlanHost& h, uint32_t Sl);
+// The 8-bit lane-serial list kernel (scl_char_kernel.hip), likewise (scl_char_rtc_kernel[_f32]).
+std::string sclc_rtc_source(const PlanHost& h, uint32_t lp, uint32_t Sl);
 // sclls_kernel.hip (host part): "#define PCG_LS_... <value>" lines of that translation unit's
 // compile-time knobs; *nondefault = a knob differs from the source's default (a dev build)
 std::string sclls_rtc_defines(bool* nondefault);

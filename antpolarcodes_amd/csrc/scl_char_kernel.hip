@@ -32,8 +32,10 @@
 #include "wave.hpp"
 #include "i8_common.hpp"
 
+#ifndef PCG_RTC
 #include <stdio.h>
 #include <stdlib.h>
+#endif
 
 namespace pcg {
 
@@ -521,7 +523,7 @@ PCG_DEV void op_branch(Wave<LP, I8>& w, uint32_t kind, uint32_t s, uint32_t o, u
 }
 
 template <int LP, bool I8>
-__global__ void __launch_bounds__(64) scl_char_kernel(KernelArgs a, uint32_t Sl)
+PCG_DEV void sclc_body(const KernelArgs& a, uint32_t Sl)
 {
     extern __shared__ uint32_t smem_u[];
     constexpr uint32_t G = 64 / LP;
@@ -669,6 +671,35 @@ __global__ void __launch_bounds__(64) scl_char_kernel(KernelArgs a, uint32_t Sl)
     }
 }
 
+#ifdef PCG_RTC
+// the plan-specialised 8-bit list decoder (rtc.cpp sclc_rtc_source): the plan's constants and
+// layout as literals, the schedule loop kept
+template <bool I8>
+PCG_DEV void sclc_rtc(const KernelArgs& a)
+{
+    KernelArgs b = a;
+    b.N = PCG_RTC_N;
+    b.log2N = PCG_RTC_LOG2N;
+    b.K = PCG_RTC_K;
+    b.kb = (PCG_RTC_K + 7u) / 8u;
+    b.L = PCG_RTC_L;
+    b.crc_bits = PCG_RTC_CRC;
+    b.systematic = PCG_RTC_SYS;
+    b.nops = PCG_RTC_NOPS;
+    sclc_body<PCG_RTC_LP, I8>(b, PCG_RTC_SL);
+}
+} // namespace
+
+extern "C" __global__ void __launch_bounds__(64) scl_char_rtc_kernel(KernelArgs a) { sclc_rtc<true>(a); }
+extern "C" __global__ void __launch_bounds__(64) scl_char_rtc_kernel_f32(KernelArgs a) { sclc_rtc<false>(a); }
+
+#else
+template <int LP, bool I8>
+__global__ void __launch_bounds__(64) scl_char_kernel(KernelArgs a, uint32_t Sl)
+{
+    sclc_body<LP, I8>(a, Sl);
+}
+
 template <int LP, bool I8>
 int resident(uint32_t lds_bytes)
 {
@@ -765,5 +796,7 @@ int launch_scl_char(const KernelArgs& a, hipStream_t stream)
 #undef PCG_SCLC_LAUNCH
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
+
+#endif // PCG_RTC
 
 } // namespace pcg

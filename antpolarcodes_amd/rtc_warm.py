@@ -27,7 +27,9 @@ def bench_codes():
         (1024, 8, ("BB", 512), 8, True, "adaptive"),  # config 3 with AdaptiveFloat (both stages)
         (1024, 8, ("5G", 512), 11, True),    # config 4
         (4096, 32, ("BB", 2048), 8, True),   # config 5
-        (1024, 1, ("BB", 512), 8, True, "char"),      # sc_char, and adaptive8_char's first stage
+        (1024, 1, ("BB", 512), 8, True, "char"),      # sc_char
+        (1024, 8, ("BB", 512), 8, True, "char"),      # scl8_char
+        (1024, 8, ("BB", 512), 8, True, "adaptive_char"),  # adaptive8_char (both stages)
     ]
 
 
@@ -60,6 +62,11 @@ def test_codes():
             out.append((N, 1, ("set", tuple(int(v) for v in fr)), crc, sysm, "char"))
     except ImportError:
         pass
+    for N, K, L, crc, sysm in ((256, 128, 2, 8, True), (1024, 512, 8, 8, True), (512, 256, 4, 16, False),
+                               (1024, 512, 16, 32, True), (1024, 512, 32, 8, True), (1024, 512, 6, 0, True)):
+        out.append((N, L, ("BB", K), crc, sysm, "char"))  # test_gpu_char.py::test_sclc_rtc_kernel
+    for crc in (8, 16):                                   # test_adaptive_char_matches_oracle
+        out.append((1024, 8, ("BB", 512), crc, True, "adaptive_char"))
     return out
 
 
@@ -79,8 +86,8 @@ def codes():
 def _one(c):
     """Compile one code in a child process (hiprtc state stays out of the caller)."""
     N, L, (kind, arg), crc, sysm = c[:5]
-    adaptive = len(c) > 5 and c[5] == "adaptive"
-    fixed = len(c) > 5 and c[5] == "char"
+    adaptive = len(c) > 5 and c[5] in ("adaptive", "adaptive_char")
+    fixed = len(c) > 5 and c[5] in ("char", "adaptive_char")
     prog = (
         "import sys; sys.path.insert(0, %r)\n"
         "from antpolarcodes_amd._native import Plan, PcgError\n"

@@ -208,9 +208,11 @@ def test_sclc_layout_variants(oracle, monkeypatch):
         _check(oracle, 1024, 8, fr, x8)
 
 
+@pytest.mark.parametrize("kernel", ["interp", "rtc"])
 @pytest.mark.parametrize("crc", [8, 16])
-def test_adaptive_char_matches_oracle(oracle, crc):
-    """AdaptiveChar (adaptive_char.cpp:33-45): FastSscFipChar, SclFipChar for the failures."""
+def test_adaptive_char_matches_oracle(oracle, crc, kernel):
+    """AdaptiveChar (adaptive_char.cpp:33-45): FastSscFipChar, SclFipChar for the failures --
+    on the interpreter kernels and on both stages' specialised kernels."""
     from antpolarcodes_amd._native import Plan
     N, L = 1024, 8
     fr = frozen_bits(N, 512, 0.0)
@@ -222,6 +224,9 @@ def test_adaptive_char_matches_oracle(oracle, crc):
     eok = np.where(sok == 1, sok, lok)
     assert (sok == 0).sum() > 10  # the list stage runs
     p = Plan(N, L, fr, crc=crc, device=0, fixed=True, adaptive=True)
+    if kernel == "rtc":
+        p.specialize()
+        assert p.describe()["specialized"] == 1 and p.kernel_name() == "scl_char_rtc_kernel"
     gi, gok, _ = p.decode_host_i8(x8)
     assert np.array_equal(gi, exp) and np.array_equal(gok, eok)
     gi, gok, _ = p.decode_host(llr * 10.0)  # float frames, quantised in the kernels
@@ -275,3 +280,28 @@ def test_scc_rtc_config_batch(oracle):
     oi, ook = oracle.scc_decode(1024, fr, x, True, 8)
     assert np.array_equal(gi, oi) and np.array_equal(gok, ook)
     assert np.array_equal(gi0, oi) and np.array_equal(gok0, ook)
+
+
+@pytest.mark.parametrize("N,K,L,crc,systematic", [(256, 128, 2, 8, True), (1024, 512, 8, 8, True),
+                                                  (512, 256, 4, 16, False), (1024, 512, 16, 32, True),
+                                                  (1024, 512, 32, 8, True), (1024, 512, 6, 0, True)])
+def test_sclc_rtc_kernel(oracle, N, K, L, crc, systematic):
+    """The 8-bit list decoder on its plan-specialised kernel (scl_char_rtc_kernel: constants
+    and layout as literals): int8 frames of every family and float frames quantised in the
+    kernel -- info, ok and the integer path metrics bit-exact against the oracle."""
+    from antpolarcodes_amd._native import Plan
+    rng = np.random.default_rng(N + L)
+    fr = frozen_bits(N, K, 0.0)
+    p = Plan(N, L, fr, systematic=systematic, crc=crc, device=0, fixed=True)
+    p.specialize()
+    assert p.kernel_name() == "scl_char_rtc_kernel" and p.describe()["specialized"] == 1
+    for kind in KINDS:
+        x = i8_kinds(rng, 48, N, kind)
+        gi, gok, gm = p.decode_host_i8(x, want_metrics=True)
+        oi, ook, om, _, _ = oracle.sclc_decode(N, L, fr, x, systematic, crc, paths=True)
+        assert np.array_equal(gi, oi) and np.array_equal(gok, ook), kind
+        assert np.array_equal(gm, om.astype(np.float32)), kind
+    llr, _, _ = frames.awgn_frames(N, fr, 256, 1.5, seed=L, crc=crc, systematic=systematic)
+    gi, gok, gm = p.decode_host(llr, want_metrics=True)
+    oi, ook, om, _, _ = oracle.sclc_decode(N, L, fr, llr, systematic, crc, paths=True)
+    assert np.array_equal(gi, oi) and np.array_equal(gok, ook) and np.array_equal(gm, om.astype(np.float32))

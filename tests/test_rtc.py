@@ -45,18 +45,23 @@ def test_specialize_compiles_list_plan(oracle):
     assert p.kernel_name() == "scl_rtc_kernel"
 
 
-def test_specialize_unsupported_plans(oracle):
-    """The 8-bit list decoder has no specialised kernel; the 8-bit Fast-SSC one has (its
-    constants and layout as literals: sccs_rtc_kernel for int8 LLRs, sccs_rtc_kernel_f32 for
-    float ones)."""
+def test_specialize_8bit_and_unsupported_plans(oracle, monkeypatch):
+    """The 8-bit decoders specialise too (their constants and layout as literals:
+    sccs_rtc_kernel / scl_char_rtc_kernel for int8 LLRs, *_f32 for float ones); a plan built
+    with the op profiler has no specialised kernel."""
     from antpolarcodes_amd._native import PcgError, PCG_E_UNSUPPORTED
-    with pytest.raises(PcgError) as e:
-        _host_plan(oracle, 256, 128, L=8, fixed=True).specialize()
-    assert e.value.code == PCG_E_UNSUPPORTED
     p = _host_plan(oracle, 256, 128, fixed=True)
     assert p.kernel_name() == "sccs_kernel"
     p.specialize()
     assert p.kernel_name() == "sccs_rtc_kernel"
+    p = _host_plan(oracle, 256, 128, L=8, fixed=True)
+    assert p.kernel_name() == "scl_char_kernel<8>"
+    p.specialize()
+    assert p.kernel_name() == "scl_char_rtc_kernel"
+    monkeypatch.setenv("PCG_OPPROF", "1")
+    with pytest.raises(PcgError) as e:
+        _host_plan(oracle, 256, 128).specialize()
+    assert e.value.code == PCG_E_UNSUPPORTED
 
 
 def _run(code, env_extra, timeout=600):
