@@ -313,6 +313,8 @@ struct VirtSt {
 // (virt = 2 is only planned when no leaf sits at stage top-2 or above: sclls_layout.)
 
 // prefetch depth (float4 chunks per batch) of the streaming loops for a storage
+// (Measured round 4, statically: 8 for the global slab's F / G -- one round trip fewer for a
+// stage-7 G -- takes the SCL-8 kernel from 252 VGPRs to 256 with 103 spilled.)
 template <typename S>
 struct Pre {
     static constexpr int U = 4;
@@ -1393,6 +1395,9 @@ PCG_DEV void weak_fast(Src src, uint32_t sl, uint32_t n, uint32_t kk, float (&T)
 #ifndef PCG_WEAK_K32
 #define PCG_WEAK_K32 1
 #endif
+#ifndef PCG_WEAK_K32_LP
+#define PCG_WEAK_K32_LP 8
+#endif
 template <int LP, int KEEP, typename Src>
 PCG_DEV bool weak_keys(Src src, uint32_t sl, uint32_t n, uint32_t kk, float (&T)[4], uint32_t (&I)[4],
                        uint32_t& par)
@@ -1645,6 +1650,10 @@ PCG_DEV uint64_t xpart64(uint64_t k)
 }
 PCG_DEV uint64_t kmax(uint64_t a, uint64_t b) { return b > a ? b : a; }
 PCG_DEV uint64_t kmin(uint64_t a, uint64_t b) { return b > a ? a : b; }
+// low ? max(k, o) : min(k, o): one compare, the lane's direction applied to its mask (SALU),
+// one select per dword -- instead of both extrema and a third select (equal keys: either)
+PCG_DEV uint64_t kdir(uint64_t k, uint64_t o, bool low) { return (o > k) == low ? o : k; }
+PCG_DEV uint32_t kdir32(uint32_t k, uint32_t o, bool low) { return (o > k) == low ? o : k; }
 
 template <int K, int D> // half-cleaner stages at lane distances D, D/2, .., 1
 PCG_DEV void bit_lanes(uint64_t (&k)[8], uint32_t p)
@@ -1653,8 +1662,7 @@ PCG_DEV void bit_lanes(uint64_t (&k)[8], uint32_t p)
         const bool low = (p & D) == 0;
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            const uint64_t o = xpart64<D>(k[j]);
-            k[j] = low ? kmax(k[j], o) : kmin(k[j], o);
+            k[j] = kdir(k[j], xpart64<D>(k[j]), low);
         }
         bit_lanes<K, D / 2>(k, p);
     }
@@ -1681,7 +1689,7 @@ PCG_DEV void bit_level(uint64_t (&k)[8], uint32_t p)
             t[j] = mirror64<2 * B>(k[K - 1 - j]);
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            k[j] = low ? kmax(k[j], t[j]) : kmin(k[j], t[j]);
+            k[j] = kdir(k[j], t[j], low);
         bit_lanes<K, B / 2>(k, p);
         bit_regs<K, K / 2>(k);
         bit_level<LP, K, 2 * B>(k, p);
@@ -1760,8 +1768,7 @@ PCG_DEV void bit_lanes32(uint32_t (&k)[8], uint32_t p)
         const bool low = (p & D) == 0;
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            const uint32_t o = xpartner<D>(k[j]);
-            k[j] = low ? umax32(k[j], o) : (k[j] > o ? o : k[j]);
+            k[j] = kdir32(k[j], xpartner<D>(k[j]), low);
         }
         bit_lanes32<K, D / 2>(k, p);
     }
@@ -1788,7 +1795,7 @@ PCG_DEV void bit_level32(uint32_t (&k)[8], uint32_t p)
             t[j] = mirror_lane<2 * B>(k[K - 1 - j]);
 #pragma unroll
         for (int j = 0; j < K; ++j)
-            k[j] = low ? umax32(k[j], t[j]) : (k[j] > t[j] ? t[j] : k[j]);
+            k[j] = kdir32(k[j], t[j], low);
         bit_lanes32<K, B / 2>(k, p);
         bit_regs32<K, K / 2>(k);
         bit_level32<LP, K, 2 * B>(k, p);
@@ -2078,7 +2085,7 @@ PCG_DEV void ls_branch_leaf(Ls<LP>& c, Src src, uint32_t code, uint32_t s, uint3
         par = fbits(a.x);
 #else
         bool done = false;
-        if constexpr (PCG_WEAK_K32 && LP <= 8) // (LP = 32 is at its register limit)
+        if constexpr (PCG_WEAK_K32 && LP <= PCG_WEAK_K32_LP) // (LP = 32 is at its register limit)
             done = kk == 2u ? weak_keys<LP, 3>(src, sl, n, kk, T, I, par) : weak_keys<LP, 5>(src, sl, n, kk, T, I, par);
         if (!done) {
             bool tie;
@@ -2863,6 +2870,7 @@ std::string sclls_rtc_defines(bool* nondefault)
     d("PCG_SEL_VMERGE", PCG_SEL_VMERGE, 0);
     d("PCG_SEL_K32", PCG_SEL_K32, 1);
     d("PCG_WEAK_K32", PCG_WEAK_K32, 1);
+    d("PCG_WEAK_K32_LP", PCG_WEAK_K32_LP, 8);
     d("PCG_LS_MINW", PCG_LS_MINW, 2);
 #ifdef PCG_LS_FULL_LOCAL_SORT
     s += "#define PCG_LS_FULL_LOCAL_SORT 1\n";
