@@ -1396,7 +1396,7 @@ PCG_DEV void weak_fast(Src src, uint32_t sl, uint32_t n, uint32_t kk, float (&T)
 #define PCG_WEAK_K32 1
 #endif
 #ifndef PCG_WEAK_K32_LP
-#define PCG_WEAK_K32_LP 8
+#define PCG_WEAK_K32_LP 32
 #endif
 template <int LP, int KEEP, typename Src>
 PCG_DEV bool weak_keys(Src src, uint32_t sl, uint32_t n, uint32_t kk, float (&T)[4], uint32_t (&I)[4],
@@ -2085,7 +2085,7 @@ PCG_DEV void ls_branch_leaf(Ls<LP>& c, Src src, uint32_t code, uint32_t s, uint3
         par = fbits(a.x);
 #else
         bool done = false;
-        if constexpr (PCG_WEAK_K32 && LP <= PCG_WEAK_K32_LP) // (LP = 32 is at its register limit)
+        if constexpr (PCG_WEAK_K32 && LP <= PCG_WEAK_K32_LP) // (config 5: +4 %, r04j_scl32_weak_k32_ab)
             done = kk == 2u ? weak_keys<LP, 3>(src, sl, n, kk, T, I, par) : weak_keys<LP, 5>(src, sl, n, kk, T, I, par);
         if (!done) {
             bool tie;
@@ -2870,7 +2870,7 @@ std::string sclls_rtc_defines(bool* nondefault)
     d("PCG_SEL_VMERGE", PCG_SEL_VMERGE, 0);
     d("PCG_SEL_K32", PCG_SEL_K32, 1);
     d("PCG_WEAK_K32", PCG_WEAK_K32, 1);
-    d("PCG_WEAK_K32_LP", PCG_WEAK_K32_LP, 8);
+    d("PCG_WEAK_K32_LP", PCG_WEAK_K32_LP, 32);
     d("PCG_LS_MINW", PCG_LS_MINW, 2);
 #ifdef PCG_LS_FULL_LOCAL_SORT
     s += "#define PCG_LS_FULL_LOCAL_SORT 1\n";
