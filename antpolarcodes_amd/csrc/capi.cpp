@@ -559,6 +559,8 @@ static int plan_create_impl(pcg_plan** out,
         if (nd) // a dev build of the list kernel (tools/build_dev_lib.sh -D...)
             p->dev_overrides |= PCG_DEV_BUILD;
     }
+    if (getenv("PCG_RTC_XOPTS")) // extra compiler options for the specialised kernels
+        p->dev_overrides |= PCG_DEV_BUILD;
     if (const char* e = getenv("PCG_RTC_SCL"); e && e[0] == '0') {
         p->rtc_scl = false;
         p->dev_overrides |= PCG_DEV_LAYOUT;

@@ -127,6 +127,30 @@ const char* const g_opts[] = {"--offload-arch=" PCG_ARCH, "-O3", "-std=c++17", "
                               "-fno-gpu-flush-denormals-to-zero", "-fno-fast-math"};
 constexpr int g_nopts = (int)(sizeof(g_opts) / sizeof(g_opts[0]));
 
+// development aid: PCG_RTC_XOPTS = extra hiprtc options, separated by spaces or commas (compiler flag A/Bs;
+// part of the cache name, and a plan compiled with them reports PCG_DEV_BUILD)
+const std::vector<std::string>& extra_opts()
+{
+    static const std::vector<std::string> v = [] {
+        std::vector<std::string> r;
+        if (const char* e = getenv("PCG_RTC_XOPTS")) {
+            std::string cur;
+            for (const char* q = e;; ++q) {
+                if (*q == ' ' || *q == ',' || *q == 0) {
+                    if (!cur.empty())
+                        r.push_back(cur);
+                    cur.clear();
+                    if (*q == 0)
+                        break;
+                } else
+                    cur += *q;
+            }
+        }
+        return r;
+    }();
+    return v;
+}
+
 uint64_t fnv1a(uint64_t h, const char* p, size_t n)
 {
     for (size_t i = 0; i < n; ++i)
@@ -151,6 +175,8 @@ std::string cache_name(const std::string& src)
     }
     for (int i = 0; i < g_nopts; ++i)
         h = fnv1a(h, g_opts[i], strlen(g_opts[i]) + 1);
+    for (const std::string& o : extra_opts())
+        h = fnv1a(h, o.c_str(), o.size() + 1);
     const std::string tag = std::string(PCG_ARCH) + "|hiprtc " + api().version;
     h = fnv1a(h, tag.data(), tag.size());
     char name[40];
@@ -269,7 +295,10 @@ int hiprtc_build(const std::string& src, std::vector<char>* code, std::string* e
         *err = "hiprtcCreateProgram failed";
         return -1;
     }
-    const hiprtcResult r = a.compile(prog, g_nopts, const_cast<const char**>(g_opts));
+    std::vector<const char*> opts(g_opts, g_opts + g_nopts);
+    for (const std::string& o : extra_opts())
+        opts.push_back(o.c_str());
+    const hiprtcResult r = a.compile(prog, (int)opts.size(), opts.data());
     if (r != HIPRTC_SUCCESS) {
         size_t n = 0;
         std::string log;
