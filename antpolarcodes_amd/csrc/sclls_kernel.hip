@@ -1742,6 +1742,9 @@ PCG_DEV uint64_t bit_pick(const uint64_t (&k)[8], uint32_t p, uint32_t gb, uint3
 #ifndef PCG_SEL_K32
 #define PCG_SEL_K32 1
 #endif
+#ifndef PCG_SEL_K32_LP
+#define PCG_SEL_K32_LP 8 // widest list on the 32-bit keys
+#endif
 PCG_DEV uint32_t ordz(float v)
 {
     const uint32_t o = ord_of(v);
@@ -1936,7 +1939,7 @@ PCG_DEV void ls_select(const Ls<LP>& c, const float (&cv)[8], uint32_t P, uint32
     const uint32_t C = P * K;
     const bool act = c.p < P;
     const uint32_t R = C > np ? np + 1 : C;
-    if constexpr (PCG_SEL_K32 && LP <= 8) { // (LP = 32: 8 code bits leave near ties common, and the
+    if constexpr (PCG_SEL_K32 && LP <= PCG_SEL_K32_LP) { // (LP = 32: 8 code bits leave near ties common, and the
                                               // 32-bit network beside the exact one spills: 1.12e6 ->
                                               // 6.7e5 cw/s on config 5, profiles/r04g_*)
         if (k32_select<LP, K>(c, cv, P, np, R, val, src, jsel)) {
@@ -2869,6 +2872,7 @@ std::string sclls_rtc_defines(bool* nondefault)
     d("PCG_SEL_BITONIC_K", PCG_SEL_BITONIC_K, 4);
     d("PCG_SEL_VMERGE", PCG_SEL_VMERGE, 0);
     d("PCG_SEL_K32", PCG_SEL_K32, 1);
+    d("PCG_SEL_K32_LP", PCG_SEL_K32_LP, 8);
     d("PCG_WEAK_K32", PCG_WEAK_K32, 1);
     d("PCG_WEAK_K32_LP", PCG_WEAK_K32_LP, 32);
     d("PCG_LS_MINW", PCG_LS_MINW, 2);
