@@ -131,7 +131,8 @@ def test_shipped_cache_holds_the_benchmark_codes():
     code = ("from antpolarcodes_amd.rtc_warm import bench_codes\n"
             "for N, L, (kind, K), crc, sysm, *ad in bench_codes():\n"
             "    p = Plan(N, L, frozen_bits(N, K, 0.0, kind), systematic=sysm, crc=crc, device=-1,\n"
-            "             adaptive=bool(ad))\n"
+            "             adaptive=ad[:1] in (['adaptive'], ['adaptive_char']),\n"
+            "             fixed=ad[:1] in (['char'], ['adaptive_char']))\n"
             "    p.specialize()\n"
             "print('compiles', lib().pcg_dev_rtc_compiles())\n")
     assert "compiles 0" in _run(code, {"PCG_RTC_CACHE": "0"}, timeout=120)
@@ -143,3 +144,17 @@ def test_dev_build_knobs_reach_the_specialised_source():
     code = ("p = Plan(1024, 8, frozen_bits(1024, 512, 0.0, 'BB'), crc=8, device=-1)\n"
             "print('dev', p.describe()['dev_overrides'])\n")
     assert "dev 0" in _run(code, {})
+
+
+def test_extra_compiler_options_are_a_dev_build(tmp_path):
+    """PCG_RTC_XOPTS (extra hiprtc options, a development aid) changes the cache name -- a
+    code object built with them is never taken for the default one -- and marks the plan's
+    results as a development build (PCG_DEV_BUILD)."""
+    code = _SMALL + "p.specialize()\nprint('dev', p.describe()['dev_overrides'])\n"
+    out = _run(code, {"PCG_RTC_CACHE": str(tmp_path / "a")})
+    assert "dev 0" in out
+    out = _run(code, {"PCG_RTC_CACHE": str(tmp_path / "b"), "PCG_RTC_XOPTS": "-mllvm,-amdgpu-schedule-metric-bias=0"})
+    assert "dev %d" % 0x40 in out
+    a = [f.name for f in (tmp_path / "a").glob("pcg_*.co")]
+    b = [f.name for f in (tmp_path / "b").glob("pcg_*.co")]
+    assert len(a) == 1 and len(b) == 1 and a != b
