@@ -471,6 +471,9 @@ def main(argv=None):
         roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": kernel, "kernel_ms": kern_ms,
                 "frames_per_launch": F, "algorithmic_bytes_per_codeword": bytes_per_cw}
+        if adaptive:  # the events bracket the whole adaptive decode, not the list kernel alone
+            roof["kernel_ms_scope"] = ("the whole adaptive decode: the Fast-SSC stage, the compaction of its CRC "
+                                       f"failures and {kernel} (rocprof gives each kernel's own average)")
         line = {
             "metric": HEADLINE_METRIC if args.mode == "scl8" else f"codewords/s ({args.mode})",
             "value": value,
