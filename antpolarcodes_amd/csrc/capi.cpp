@@ -11,8 +11,10 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
+struct HostPipe;
 struct pcg_plan {
     pcg::PlanHost host;
     int device = 0;
@@ -45,6 +47,9 @@ struct pcg_plan {
     uint8_t* d_ok = nullptr;
     float* d_met = nullptr;
     uint64_t stage_frames = 0;
+    // host-pointer pipeline (pcg_decode_f32_host / _i8_host): two chunk slots, each with device
+    // buffers and pinned host staging, a copy stream and a decode stream (HostPipe below)
+    struct HostPipe* pipe = nullptr;
     // pcg_decode_punctured_f32: depunctured LLRs (F x N), reused across calls
     float* d_dep = nullptr;
     uint64_t dep_frames = 0;
@@ -80,6 +85,24 @@ struct pcg_plan {
     hipModule_t rtc_mod = nullptr;
     hipFunction_t rtc_fn = nullptr;
     hipFunction_t rtc_fn_i8 = nullptr; // 8-bit plans: the kernel for int8 channel LLRs (rtc_fn: float LLRs)
+};
+
+// The host-pointer pipeline of pcg_decode_f32_host / pcg_decode_i8_host: chunks of the
+// caller's batch alternate between two slots, so chunk i+1's host staging and H2D copy (copy
+// stream) run while chunk i decodes (decode stream) and chunk i-1's outputs come back.
+struct HostPipe {
+    hipStream_t copy = nullptr, dec = nullptr;
+    uint64_t frames = 0; // capacity of a slot in frames
+    size_t in_fb = 0;    // input bytes per frame the slots were sized for
+    uint32_t L = 0;
+    uint64_t kb = 0;
+    void* d_in[2] = {nullptr, nullptr};
+    uint8_t* d_info[2] = {nullptr, nullptr};
+    uint8_t* d_ok[2] = {nullptr, nullptr};
+    float* d_met[2] = {nullptr, nullptr};
+    void* h_in[2] = {nullptr, nullptr};     // pinned input staging (mode 2)
+    uint8_t* h_out[2] = {nullptr, nullptr}; // pinned outputs of one chunk: info | ok | metrics
+    hipEvent_t ev_h2d[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
 };
 
 namespace {
@@ -128,11 +151,39 @@ struct DeviceGuard {
     }
 };
 
+void free_pipe(HostPipe* q)
+{
+    if (!q)
+        return;
+    for (hipStream_t st : {q->copy, q->dec})
+        if (st) {
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
+        }
+    for (int b = 0; b < 2; ++b) {
+        (void)hipFree(q->d_in[b]);
+        (void)hipFree(q->d_info[b]);
+        (void)hipFree(q->d_ok[b]);
+        (void)hipFree(q->d_met[b]);
+        if (q->h_in[b])
+            (void)hipHostFree(q->h_in[b]);
+        if (q->h_out[b])
+            (void)hipHostFree(q->h_out[b]);
+        if (q->ev_h2d[b])
+            (void)hipEventDestroy(q->ev_h2d[b]);
+        if (q->ev_done[b])
+            (void)hipEventDestroy(q->ev_done[b]);
+    }
+    delete q;
+}
+
 void free_plan_device(pcg_plan* p)
 {
     // everything queued on the plan's buffers has finished once its last event has
     if (p->has_last)
         (void)hipEventSynchronize(p->last_ev);
+    free_pipe(p->pipe);
+    p->pipe = nullptr;
     (void)hipFree(p->d_ops);
     (void)hipFree(p->d_info_pos);
     (void)hipFree(p->d_crc_m);
@@ -165,11 +216,11 @@ void free_plan_device(pcg_plan* p)
 constexpr uint64_t RTC_AUTO_FRAMES = 8192;
 
 // Plans with a specialised kernel: Fast-SSC float plans on the LDS-resident kernel (the walk
-// unrolled) and float list plans (their layout and plan constants as literals, the schedule
+// unrolled), float list plans (their layout and plan constants as literals, the schedule
 // loop kept: a fully unrolled walk -- 280 schedule words for config 3, each op inlining path
 // selection and the leaf decoders -- had not compiled after 20 minutes, against 34 s for
-// config 2's 60 fused Fast-SSC ops; PCG_RTC_SCL=0 keeps list plans on the interpreter), not
-// an adaptive plan's list stage (a few frames per launch); never with the op profiler.
+// config 2's 60 fused Fast-SSC ops; PCG_RTC_SCL=0 keeps list plans on the interpreter), the
+// 8-bit lane-serial kernels, and both stages of adaptive plans; never with the op profiler.
 bool rtc_capable(const pcg_plan* p)
 {
     if (p->dev_opprof)
@@ -774,8 +825,8 @@ int pcg_plan_describe(const pcg_plan* p, pcg_plan_desc* d)
                           : (p->host.L == 1 && p->host.sc_kind == 2 ? p->host.scq_q : 0);
     d->dev_overrides = p->dev_overrides | (p->fast ? p->fast->dev_overrides : 0u);
     d->recomputed_stages = p->host.L > 1 && !p->host.fixed ? p->scl_virt : 0u;
-    // every stage that has a specialised kernel runs it (an adaptive plan: both stages; the
-    // 8-bit one: its Fast-SSC stage, the 8-bit list stage has none)
+    // every stage that has a specialised kernel runs it (an adaptive plan: both stages, float
+    // and 8-bit alike)
     {
         bool any = false, all = true;
         for (const pcg_plan* q : {(const pcg_plan*)p->fast, p})
@@ -1022,6 +1073,218 @@ int pcg_decode_i8(pcg_plan* p,
     return decode_impl(p, nullptr, F, info, ok, metrics, stream, nullptr, nullptr, llr);
 }
 
+// ---- host-pointer decodes: the overlapped pipeline ----------------------------------------
+// Reference callers: Decoder::decode_vector (decoder.cpp:154-181), pypolar decode on numpy
+// arrays (python/bindings/decoder_python.cc:41-75), the simulator's block loop
+// (simulator.cpp:920-937) -- all hand over host buffers.  The batch is cut into chunks that
+// alternate between two slots (HostPipe): the host stages chunk i+1 and the copy stream
+// moves it to the device while the decode stream decodes chunk i, whose (small) outputs come
+// back on the decode stream into pinned memory and are handed to the caller when the slot
+// is reused.  PCG_HOST_PIPE selects the staging (development A/B; default 2):
+//   0  serial: blocking pageable copies, then the decode, chunk by chunk (no overlap);
+//   1  the caller's pageable buffer copied by the runtime on the copy stream (the host thread
+//      blocks in the copy while the previous chunk decodes);
+//   2  plan-owned pinned staging filled by PCG_HOST_THREADS host threads (default 8), then a
+//      DMA copy on the copy stream.
+// A caller buffer that is already pinned (hipHostMalloc / hipHostRegister) is copied from
+// directly in modes 1 and 2.  PCG_HOST_CHUNK overrides the chunk size in frames (default:
+// 64 MB of input, between 4096 and 65536 frames).
+static int env_int(const char* name, int dflt)
+{
+    const char* e = getenv(name);
+    return e && *e ? atoi(e) : dflt;
+}
+
+static void par_memcpy(void* dst, const void* src, size_t bytes, int threads)
+{
+    const size_t per = size_t(4) << 20; // at least 4 MB per thread
+    int t = (int)std::min<size_t>((size_t)std::max(threads, 1), (bytes + per - 1) / per);
+    if (t <= 1) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    const size_t part = ((bytes + t - 1) / t + 4095) & ~size_t(4095);
+    std::vector<std::thread> th;
+    for (int k = 1; k < t; ++k) {
+        const size_t o = part * k;
+        if (o >= bytes)
+            break;
+        th.emplace_back([=] { memcpy((char*)dst + o, (const char*)src + o, std::min(part, bytes - o)); });
+    }
+    memcpy(dst, src, std::min(part, bytes));
+    for (auto& x : th)
+        x.join();
+}
+
+static int pipe_alloc(pcg_plan* p, uint64_t frames, size_t in_fb, bool pinned_in)
+{
+    HostPipe* q = p->pipe;
+    const auto& h = p->host;
+    if (q && q->frames >= frames && q->in_fb >= in_fb && (!pinned_in || q->h_in[0]))
+        return PCG_OK;
+    if (q) { // grow: everything queued on the old buffers finishes first
+        frames = std::max(frames, q->frames);
+        in_fb = std::max(in_fb, q->in_fb);
+        pinned_in = pinned_in || q->h_in[0];
+        free_pipe(q);
+        p->pipe = nullptr;
+    }
+    q = new HostPipe;
+    p->pipe = q;
+    q->frames = frames;
+    q->in_fb = in_fb;
+    q->L = h.L;
+    q->kb = std::max<uint64_t>((h.K + 7) / 8, 1);
+    hipError_t e;
+    if ((e = hipStreamCreateWithFlags(&q->copy, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipStreamCreateWithFlags(&q->dec, hipStreamNonBlocking)) != hipSuccess)
+        return hip_fail(e, "hipStreamCreate(host pipeline)");
+    const size_t out_b = frames * (q->kb + 1 + h.L * sizeof(float));
+    for (int b = 0; b < 2; ++b) {
+        if ((e = hipMalloc(&q->d_in[b], frames * in_fb)) != hipSuccess ||
+            (e = hipMalloc(&q->d_info[b], frames * q->kb)) != hipSuccess ||
+            (e = hipMalloc(&q->d_ok[b], frames)) != hipSuccess ||
+            (e = hipMalloc(&q->d_met[b], frames * h.L * sizeof(float))) != hipSuccess)
+            return hip_fail(e, "hipMalloc(host pipeline)");
+        if ((e = hipHostMalloc(&q->h_out[b], out_b, hipHostMallocDefault)) != hipSuccess)
+            return hip_fail(e, "hipHostMalloc(host pipeline outputs)");
+        if (pinned_in && (e = hipHostMalloc(&q->h_in[b], frames * in_fb, hipHostMallocDefault)) != hipSuccess)
+            return hip_fail(e, "hipHostMalloc(host pipeline staging)");
+        if ((e = hipEventCreateWithFlags(&q->ev_h2d[b], hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&q->ev_done[b], hipEventDisableTiming)) != hipSuccess)
+            return hip_fail(e, "hipEventCreate(host pipeline)");
+    }
+    return PCG_OK;
+}
+
+// the caller's buffer is page-locked host memory the DMA engines can read directly
+static bool host_pinned(const void* ptr)
+{
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, ptr) != hipSuccess) {
+        (void)hipGetLastError(); // (pageable memory: not an error worth keeping)
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
+
+static int decode_host_serial(pcg_plan* p, const void* llr, size_t elem, uint64_t F, uint8_t* info, uint8_t* ok,
+                              float* metrics, uint64_t chunk)
+{
+    const auto& h = p->host;
+    const uint64_t kb = (h.K + 7) / 8;
+    const size_t fb = h.N * elem;
+    int rc = pipe_alloc(p, chunk, fb, false);
+    if (rc != 0)
+        return rc;
+    HostPipe* q = p->pipe;
+    hipError_t e;
+    for (uint64_t f0 = 0; f0 < F; f0 += chunk) {
+        const uint64_t n = std::min(chunk, F - f0);
+        if ((e = hipMemcpy(q->d_in[0], (const char*)llr + f0 * fb, n * fb, hipMemcpyHostToDevice)) != hipSuccess)
+            return hip_fail(e, "hipMemcpy(H2D)");
+        rc = elem == 1 ? pcg_decode_i8(p, (const int8_t*)q->d_in[0], n, q->d_info[0], ok ? q->d_ok[0] : nullptr,
+                                       metrics ? q->d_met[0] : nullptr, nullptr)
+                       : pcg_decode_f32(p, (const float*)q->d_in[0], n, q->d_info[0], ok ? q->d_ok[0] : nullptr,
+                                        metrics ? q->d_met[0] : nullptr, nullptr);
+        if (rc != 0)
+            return rc;
+        if ((e = hipMemcpy(info + f0 * kb, q->d_info[0], n * kb, hipMemcpyDeviceToHost)) != hipSuccess)
+            return hip_fail(e, "hipMemcpy(D2H info)");
+        if (ok && (e = hipMemcpy(ok + f0, q->d_ok[0], n, hipMemcpyDeviceToHost)) != hipSuccess)
+            return hip_fail(e, "hipMemcpy(D2H ok)");
+        if (metrics &&
+            (e = hipMemcpy(metrics + f0 * h.L, q->d_met[0], n * h.L * sizeof(float), hipMemcpyDeviceToHost)) !=
+                hipSuccess)
+            return hip_fail(e, "hipMemcpy(D2H metrics)");
+    }
+    return PCG_OK;
+}
+
+static int decode_host(pcg_plan* p, const void* llr, size_t elem, uint64_t F, uint8_t* info, uint8_t* ok,
+                       float* metrics)
+{
+    const auto& h = p->host;
+    const uint64_t kb = (h.K + 7) / 8;
+    const size_t fb = h.N * elem;
+    const int mode = env_int("PCG_HOST_PIPE", 2);
+    uint64_t chunk = (uint64_t)env_int("PCG_HOST_CHUNK", 0);
+    if (chunk == 0)
+        chunk = std::min<uint64_t>(65536, std::max<uint64_t>(4096, (64ull << 20) / fb));
+    chunk = std::min<uint64_t>(chunk, F);
+    if (mode == 0)
+        return decode_host_serial(p, llr, elem, F, info, ok, metrics, chunk);
+    const bool direct = host_pinned(llr);
+    const bool stage = mode == 2 && !direct;
+    const int threads = env_int("PCG_HOST_THREADS", 8);
+    int rc = pipe_alloc(p, chunk, fb, stage);
+    if (rc != 0)
+        return rc;
+    HostPipe* q = p->pipe;
+    hipError_t e;
+    // the slots' buffers are reused after the plan's previous decodes, whatever stream ran them
+    if ((rc = order_on(p, q->copy)) != 0)
+        return rc;
+    struct Pending {
+        uint64_t f0 = 0, n = 0;
+        bool live = false;
+    } pend[2];
+    const size_t o_ok = chunk * kb, o_met = o_ok + chunk;
+    auto retire = [&](int b) -> int {
+        if (!pend[b].live)
+            return PCG_OK;
+        pend[b].live = false;
+        hipError_t x = hipEventSynchronize(q->ev_done[b]);
+        if (x != hipSuccess)
+            return hip_fail(x, "hipEventSynchronize(host pipeline)");
+        const uint64_t f0 = pend[b].f0, n = pend[b].n;
+        memcpy(info + f0 * kb, q->h_out[b], n * kb);
+        if (ok)
+            memcpy(ok + f0, q->h_out[b] + o_ok, n);
+        if (metrics)
+            memcpy(metrics + f0 * h.L, q->h_out[b] + o_met, n * h.L * sizeof(float));
+        return PCG_OK;
+    };
+    uint64_t i = 0;
+    for (uint64_t f0 = 0; f0 < F; f0 += chunk, ++i) {
+        const int b = (int)(i & 1u);
+        const uint64_t n = std::min(chunk, F - f0);
+        // chunk i-2 leaves slot b: its decode (and so its input copy) is complete
+        if ((rc = retire(b)) != 0)
+            return rc;
+        const char* src = (const char*)llr + f0 * fb;
+        if (stage) {
+            par_memcpy(q->h_in[b], src, n * fb, threads);
+            src = (const char*)q->h_in[b];
+        }
+        if ((e = hipMemcpyAsync(q->d_in[b], src, n * fb, hipMemcpyHostToDevice, q->copy)) != hipSuccess)
+            return hip_fail(e, "hipMemcpyAsync(H2D)");
+        if ((e = hipEventRecord(q->ev_h2d[b], q->copy)) != hipSuccess ||
+            (e = hipStreamWaitEvent(q->dec, q->ev_h2d[b], 0)) != hipSuccess)
+            return hip_fail(e, "host pipeline event");
+        rc = elem == 1 ? pcg_decode_i8(p, (const int8_t*)q->d_in[b], n, q->d_info[b], ok ? q->d_ok[b] : nullptr,
+                                       metrics ? q->d_met[b] : nullptr, q->dec)
+                       : pcg_decode_f32(p, (const float*)q->d_in[b], n, q->d_info[b], ok ? q->d_ok[b] : nullptr,
+                                        metrics ? q->d_met[b] : nullptr, q->dec);
+        if (rc != 0)
+            return rc;
+        if ((e = hipMemcpyAsync(q->h_out[b], q->d_info[b], n * kb, hipMemcpyDeviceToHost, q->dec)) != hipSuccess ||
+            (ok && (e = hipMemcpyAsync(q->h_out[b] + o_ok, q->d_ok[b], n, hipMemcpyDeviceToHost, q->dec)) !=
+                       hipSuccess) ||
+            (metrics && (e = hipMemcpyAsync(q->h_out[b] + o_met, q->d_met[b], n * h.L * sizeof(float),
+                                            hipMemcpyDeviceToHost, q->dec)) != hipSuccess))
+            return hip_fail(e, "hipMemcpyAsync(D2H)");
+        if ((e = hipEventRecord(q->ev_done[b], q->dec)) != hipSuccess)
+            return hip_fail(e, "hipEventRecord(host pipeline)");
+        pend[b] = {f0, n, true};
+    }
+    // the last two chunks, in order
+    const int last = (int)((i - 1) & 1u);
+    if ((rc = retire(last ^ 1)) != 0 || (rc = retire(last)) != 0)
+        return rc;
+    return PCG_OK;
+}
+
 int pcg_decode_i8_host(pcg_plan* p, const int8_t* llr, uint64_t F, uint8_t* info, uint8_t* ok, float* metrics)
 {
     if (!p)
@@ -1035,45 +1298,7 @@ int pcg_decode_i8_host(pcg_plan* p, const int8_t* llr, uint64_t F, uint8_t* info
     if (p->device < 0)
         return fail(PCG_E_NODEVICE, "host-only plan (created with device < 0)");
     DeviceGuard g(p->device);
-    const auto& h = p->host;
-    const uint64_t kb = (h.K + 7) / 8;
-    const uint64_t chunk = std::min<uint64_t>(F, 1u << 16);
-    hipError_t e;
-    if (p->stage_frames < chunk) { // the float staging buffer holds the int8 frames too
-        (void)hipFree(p->d_llr);
-        (void)hipFree(p->d_info);
-        (void)hipFree(p->d_ok);
-        (void)hipFree(p->d_met);
-        p->d_llr = nullptr;
-        p->d_info = nullptr;
-        p->d_ok = nullptr;
-        p->d_met = nullptr;
-        p->stage_frames = 0;
-        if ((e = hipMalloc(&p->d_llr, chunk * h.N * sizeof(float))) != hipSuccess ||
-            (e = hipMalloc(&p->d_info, chunk * std::max<uint64_t>(kb, 1))) != hipSuccess ||
-            (e = hipMalloc(&p->d_ok, chunk)) != hipSuccess ||
-            (e = hipMalloc(&p->d_met, chunk * h.L * sizeof(float))) != hipSuccess)
-            return hip_fail(e, "hipMalloc(staging)");
-        p->stage_frames = chunk;
-    }
-    int8_t* d8 = reinterpret_cast<int8_t*>(p->d_llr);
-    for (uint64_t f0 = 0; f0 < F; f0 += chunk) {
-        const uint64_t n = std::min(chunk, F - f0);
-        if ((e = hipMemcpy(d8, llr + f0 * h.N, n * h.N, hipMemcpyHostToDevice)) != hipSuccess)
-            return hip_fail(e, "hipMemcpy(H2D)");
-        int rc = pcg_decode_i8(p, d8, n, p->d_info, ok ? p->d_ok : nullptr, metrics ? p->d_met : nullptr, nullptr);
-        if (rc != 0)
-            return rc;
-        if ((e = hipMemcpy(info + f0 * kb, p->d_info, n * kb, hipMemcpyDeviceToHost)) != hipSuccess)
-            return hip_fail(e, "hipMemcpy(D2H info)");
-        if (ok && (e = hipMemcpy(ok + f0, p->d_ok, n, hipMemcpyDeviceToHost)) != hipSuccess)
-            return hip_fail(e, "hipMemcpy(D2H ok)");
-        if (metrics &&
-            (e = hipMemcpy(metrics + f0 * h.L, p->d_met, n * h.L * sizeof(float), hipMemcpyDeviceToHost)) !=
-                hipSuccess)
-            return hip_fail(e, "hipMemcpy(D2H metrics)");
-    }
-    return PCG_OK;
+    return decode_host(p, llr, 1, F, info, ok, metrics);
 }
 
 int pcg_decode_f32_host(pcg_plan* p, const float* llr, uint64_t F, uint8_t* info, uint8_t* ok, float* metrics)
@@ -1087,45 +1312,7 @@ int pcg_decode_f32_host(pcg_plan* p, const float* llr, uint64_t F, uint8_t* info
     if (p->device < 0)
         return fail(PCG_E_NODEVICE, "host-only plan (created with device < 0)");
     DeviceGuard g(p->device);
-    const auto& h = p->host;
-    const uint64_t kb = (h.K + 7) / 8;
-    const uint64_t chunk = std::min<uint64_t>(F, 1u << 16);
-    hipError_t e;
-    if (p->stage_frames < chunk) {
-        (void)hipFree(p->d_llr);
-        (void)hipFree(p->d_info);
-        (void)hipFree(p->d_ok);
-        (void)hipFree(p->d_met);
-        p->d_llr = nullptr;
-        p->d_info = nullptr;
-        p->d_ok = nullptr;
-        p->d_met = nullptr;
-        p->stage_frames = 0;
-        if ((e = hipMalloc(&p->d_llr, chunk * h.N * sizeof(float))) != hipSuccess ||
-            (e = hipMalloc(&p->d_info, chunk * std::max<uint64_t>(kb, 1))) != hipSuccess ||
-            (e = hipMalloc(&p->d_ok, chunk)) != hipSuccess ||
-            (e = hipMalloc(&p->d_met, chunk * h.L * sizeof(float))) != hipSuccess)
-            return hip_fail(e, "hipMalloc(staging)");
-        p->stage_frames = chunk;
-    }
-    for (uint64_t f0 = 0; f0 < F; f0 += chunk) {
-        const uint64_t n = std::min(chunk, F - f0);
-        if ((e = hipMemcpy(p->d_llr, llr + f0 * h.N, n * h.N * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess)
-            return hip_fail(e, "hipMemcpy(H2D)");
-        int rc = pcg_decode_f32(p, p->d_llr, n, p->d_info, ok ? p->d_ok : nullptr,
-                                metrics ? p->d_met : nullptr, nullptr);
-        if (rc != 0)
-            return rc;
-        if ((e = hipMemcpy(info + f0 * kb, p->d_info, n * kb, hipMemcpyDeviceToHost)) != hipSuccess)
-            return hip_fail(e, "hipMemcpy(D2H info)");
-        if (ok && (e = hipMemcpy(ok + f0, p->d_ok, n, hipMemcpyDeviceToHost)) != hipSuccess)
-            return hip_fail(e, "hipMemcpy(D2H ok)");
-        if (metrics &&
-            (e = hipMemcpy(metrics + f0 * h.L, p->d_met, n * h.L * sizeof(float), hipMemcpyDeviceToHost)) !=
-                hipSuccess)
-            return hip_fail(e, "hipMemcpy(D2H metrics)");
-    }
-    return PCG_OK;
+    return decode_host(p, llr, sizeof(float), F, info, ok, metrics);
 }
 
 static int soft_supported(const pcg_plan* p)

@@ -35,6 +35,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <map>
@@ -165,8 +166,10 @@ void mkdirs(const std::string& dir)
             (void)mkdir(dir.substr(0, k).c_str(), 0755);
 }
 
-// The cache file name of a generated source: everything that determines the code object.
-std::string cache_name(const std::string& src)
+// The cache file name of a generated source: everything that determines the code object
+// (ver: the hiprtc version that compiles it -- this process's, or the one the shipped cache
+// was built with).
+std::string cache_name(const std::string& src, const std::string& ver)
 {
     uint64_t h = fnv1a(0xcbf29ce484222325ull, src.data(), src.size());
     for (int i = 0; i < rtc_nsrcs; ++i) {
@@ -177,12 +180,13 @@ std::string cache_name(const std::string& src)
         h = fnv1a(h, g_opts[i], strlen(g_opts[i]) + 1);
     for (const std::string& o : extra_opts())
         h = fnv1a(h, o.c_str(), o.size() + 1);
-    const std::string tag = std::string(PCG_ARCH) + "|hiprtc " + api().version;
+    const std::string tag = std::string(PCG_ARCH) + "|hiprtc " + ver;
     h = fnv1a(h, tag.data(), tag.size());
     char name[40];
     snprintf(name, sizeof(name), "pcg_%016llx.co", (unsigned long long)h);
     return name;
 }
+std::string cache_name(const std::string& src) { return cache_name(src, api().version); }
 
 // the user cache directory, or "" when it is off
 std::string user_dir()
@@ -208,6 +212,25 @@ std::string shipped_dir()
     std::string p = info.dli_fname;
     const size_t k = p.rfind('/');
     return k == std::string::npos ? std::string("rtc") : p.substr(0, k) + "/rtc";
+}
+
+// A cache directory records the hiprtc version its files were compiled with
+// (kVersionFile): the shipped cache is looked up under the build machine's version, so a
+// machine without hiprtc (or with another version) still loads the shipped code objects --
+// they only need hipModuleLoadData.
+constexpr const char* kVersionFile = "HIPRTC_VERSION";
+std::string dir_version(const std::string& dir)
+{
+    std::string v;
+    if (FILE* f = fopen((dir + "/" + kVersionFile).c_str(), "r")) {
+        char buf[64] = {0};
+        if (fgets(buf, sizeof(buf), f))
+            v = buf;
+        fclose(f);
+    }
+    while (!v.empty() && (v.back() == '\n' || v.back() == '\r' || v.back() == ' '))
+        v.pop_back();
+    return v;
 }
 
 // File = code object, then a 24-byte trailer: "PCGRTC01", the code length, its FNV-1a hash.
@@ -242,6 +265,12 @@ bool read_file(const std::string& path, std::vector<char>* out)
 void write_file(const std::string& dir, const std::string& name, const std::vector<char>& code)
 {
     mkdirs(dir);
+    if (dir_version(dir).empty() && api().ok) { // (first writer; every writer of a version agrees)
+        if (FILE* f = fopen((dir + "/" + kVersionFile).c_str(), "w")) {
+            fprintf(f, "%s\n", api().version.c_str());
+            fclose(f);
+        }
+    }
     std::string tmpl = dir + "/." + name + ".XXXXXX";
     const int fd = mkstemp(&tmpl[0]); // unique per writer: concurrent writers never share a temp file
     if (fd < 0)
@@ -265,12 +294,14 @@ void write_file(const std::string& dir, const std::string& name, const std::vect
 // cached code object of a source: shipped, then user cache
 bool disk_lookup(const std::string& src, std::vector<char>* code)
 {
-    const std::string name = cache_name(src);
     const std::string sd = shipped_dir();
-    if (!sd.empty() && read_file(sd + "/" + name, code))
-        return true;
+    if (!sd.empty()) {
+        const std::string sv = dir_version(sd);
+        if (read_file(sd + "/" + cache_name(src, sv.empty() ? api().version : sv), code))
+            return true;
+    }
     const std::string ud = user_dir();
-    return !ud.empty() && read_file(ud + "/" + name, code);
+    return !ud.empty() && read_file(ud + "/" + cache_name(src), code);
 }
 
 void dump_source(const std::string& src)
@@ -338,16 +369,53 @@ void finish(RtcJob& j)
     j.cv.notify_all();
 }
 
-// process exit waits for compiles still running (their thread is inside hiprtc)
+// Process exit waits for compiles still running (their thread is inside hiprtc, whose
+// teardown must not run under it).  It says so on stderr when it has to wait, and
+// PCG_RTC_EXIT_WAIT=<seconds> bounds the wait: past it the process ends at once (_exit,
+// status 0: the program itself has finished) without running the remaining exit handlers.
 void wait_running()
 {
     Registry& r = reg();
     std::unique_lock<std::mutex> lk(r.mu);
     if (getenv("PCG_RTC_DEBUG"))
         fprintf(stderr, "[pcg] exit: %d compiles running\n", r.running);
-    r.idle.wait(lk, [&] { return r.running == 0; });
+    if (r.running > 0)
+        fprintf(stderr,
+                "[pcg] waiting for %d background kernel compile(s) to finish before exit "
+                "(PCG_RTC=0: no automatic compiles; PCG_RTC_EXIT_WAIT=<s>: bound this wait)\n",
+                r.running);
+    long bound = -1;
+    if (const char* e = getenv("PCG_RTC_EXIT_WAIT"))
+        bound = atol(e);
+    if (bound >= 0) {
+        if (!r.idle.wait_for(lk, std::chrono::seconds(bound), [&] { return r.running == 0; })) {
+            fprintf(stderr, "[pcg] exit: %d compile(s) still running after %ld s; leaving without them\n",
+                    r.running, bound);
+            fflush(stderr);
+            _exit(0);
+        }
+    } else {
+        r.idle.wait(lk, [&] { return r.running == 0; });
+    }
     if (getenv("PCG_RTC_DEBUG"))
         fprintf(stderr, "[pcg] exit: compiles done\n");
+}
+
+// The exit hook must run before the destructors of hiprtc's compiler (comgr, loaded by
+// hiprtc's first compile, and the function-local statics that compile creates): exit() runs
+// handlers in reverse order of registration, so a small compile runs first, then the hook
+// is registered.  Once per process, before the registry lock is taken: the first
+// rtc_start of a process blocks its caller for this warm-up (loading comgr, ~1-2 s), never
+// another thread's registry access.
+void warm_and_hook()
+{
+    static std::once_flag at;
+    std::call_once(at, [] {
+        std::vector<char> c;
+        std::string e;
+        (void)hiprtc_build(kWarmSrc, &c, &e);
+        atexit(wait_running);
+    });
 }
 
 } // namespace
@@ -465,6 +533,7 @@ std::shared_ptr<RtcJob> rtc_start(const std::string& src)
     if (auto j = rtc_lookup(src))
         return j;
     Registry& r = reg();
+    warm_and_hook();
     std::shared_ptr<RtcJob> j;
     {
         std::lock_guard<std::mutex> lk(r.mu);
@@ -473,17 +542,6 @@ std::shared_ptr<RtcJob> rtc_start(const std::string& src)
             return it->second; // another plan's compile of the same source: share it
         j = std::make_shared<RtcJob>();
         r.jobs.emplace(src, j);
-        static std::once_flag at;
-        std::call_once(at, [] {
-            // The exit hook must run before the destructors of hiprtc's compiler (comgr, loaded
-            // by hiprtc's first compile, and the function-local statics that compile creates):
-            // exit() runs handlers in reverse order of registration, so a small compile runs
-            // first, then the hook is registered.
-            std::vector<char> c;
-            std::string e;
-            (void)hiprtc_build(kWarmSrc, &c, &e);
-            atexit(wait_running);
-        });
         ++r.running;
         ++r.started;
     }

@@ -30,7 +30,10 @@ std::string sclls_rtc_defines(bool* nondefault);
 struct RtcJob;
 // Start (or join) the compile of `src`: a code object already in the process cache, the
 // library's shipped cache (<dir of libpcg.so>/rtc) or the user cache (PCG_RTC_CACHE) makes a
-// finished job at once; otherwise hiprtc runs in a detached thread.  Never blocks on hiprtc.
+// finished job at once; otherwise hiprtc runs in a detached thread.  Never waits for that
+// compile; the first one a process starts is preceded, on the caller's thread and outside any
+// lock, by a small warm-up compile that loads hiprtc's compiler (~1-2 s, once per process:
+// rtc.cpp warm_and_hook).
 std::shared_ptr<RtcJob> rtc_start(const std::string& src);
 // A finished job from the caches only, or null (no compile is started).
 std::shared_ptr<RtcJob> rtc_lookup(const std::string& src);

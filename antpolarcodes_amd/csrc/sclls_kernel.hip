@@ -2933,6 +2933,13 @@ int launch_sclls(const KernelArgs& a, hipStream_t stream)
     lds += 64 * sizeof(uint64_t);
 #endif
     const uint32_t lp = a.scl_lp > lp_of(a.L) ? a.scl_lp : lp_of(a.L);
+#if PCG_LS_INST
+    // a development build (tools/build_dev_lib.sh: this host part and one width compiled with
+    // the dev knobs): the other widths' objects were built with the default knobs, whose
+    // layout need not be the one computed here -- refused, never run on a mismatched layout
+    if (lp != PCG_LS_INST)
+        return -4;
+#endif
     switch (lp) {
     case 2: return sclls_launch_2(a, lds, stream);
     case 4: return sclls_launch_4(a, lds, stream);

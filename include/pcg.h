@@ -107,7 +107,7 @@ typedef struct pcg_plan_desc {
                                     where read instead of stored (1: the root's children, 2:
                                     also its grandchildren); 0 for the other kernels */
     uint32_t specialized;        /* 1: decodes run the plan-specialised kernel (pcg_plan_specialize;
-                                    an adaptive plan: its Fast-SSC stage) */
+                                    an adaptive plan: both of its stages) */
 } pcg_plan_desc;
 
 #define PCG_DEV_SCL_LP 0x1   /* PCG_SCL_LP / PCG_ADAPT_LP (only when the caller passed 0) */
@@ -247,25 +247,34 @@ int pcg_plan_describe(const pcg_plan* plan, pcg_plan_desc* desc);
 const char* pcg_plan_kernel_name(const pcg_plan* plan);
 
 /* Compile (hiprtc, at run time) and load a kernel specialised to this plan's code: the
- * LDS-resident Fast-SSC kernel with the plan's decoder tree as a compile-time schedule, or the
- * lane-serial list kernel with the plan's layout and constants as literals -- the same device
- * code and arithmetic as the interpreter kernels, so the same outputs bit for bit.  This
+ * LDS-resident Fast-SSC kernel with the plan's decoder tree as a compile-time schedule, the
+ * lane-serial list kernel with the plan's layout and constants as literals, and for 8-bit
+ * plans the lane-serial FastSscFipChar / SclFipChar kernels with their constants and layout as
+ * literals (sccs_rtc_kernel / scl_char_rtc_kernel) -- the same device code and arithmetic as
+ * the interpreter kernels, so the same outputs bit for bit.  An adaptive plan specialises both
+ * of its stages.  This
  * replaces the reference's per-code decoder object tree (FastSscAvx::createDecoder,
  * fastssc_avx_float.cpp:797-896; SclAvx::createDecoder, scl_avx_float.cpp:624-651) with
  * per-code machine code.  Code objects are cached per process, in the library's shipped
- * cache (<dir of libpcg.so>/rtc, filled at build time for the benchmark and test codes) and
+ * cache (<dir of libpcg.so>/rtc, filled at build time for the catalogue of
+ * antpolarcodes_amd/rtc_codes.py: the benchmark configurations and a validation catalogue) and
  * on disk (PCG_RTC_CACHE); a code in none of them takes tens of seconds of hiprtc once.
  * Plans do this by themselves: with a cached code object from their first decode, otherwise
  * in a background thread from their first decode of >= 8192 frames, switching once it is
  * ready (PCG_RTC=0 never, PCG_RTC=1 at the first decode, waiting).  PCG_E_UNSUPPORTED for
- * 8-bit plans (and with PCG_OPPROF); on a host-only plan it only compiles.  On failure (no
- * hiprtc, a device of another architecture) the plan keeps decoding with the interpreter
- * kernel.  Plans of one code share one compile; pcg_plan_destroy never waits for it (process
- * exit does). */
+ * the 8-bit Fast-SSC plans that run the one-codeword-per-wave kernel and with PCG_OPPROF; on
+ * a host-only plan it only compiles.  On failure (no hiprtc, a device of another
+ * architecture) the plan keeps decoding with the interpreter kernel.  Plans of one code
+ * share one compile; pcg_plan_destroy never waits for it, process exit does (with a notice
+ * on stderr; PCG_RTC_EXIT_WAIT=<s> bounds that wait).  The first compile a process starts is
+ * preceded by a short warm-up compile (~1-2 s, loading hiprtc's compiler) on the calling
+ * thread, so the first pcg_plan_specialize_async -- or the first decode of >= 8192 frames
+ * that starts a compile -- can block for that long. */
 int pcg_plan_specialize(pcg_plan* plan);
 
 /* Start pcg_plan_specialize without waiting: the plan switches at a later decode (or
- * pcg_plan_specialize) once the code object is ready.  Returns at once. */
+ * pcg_plan_specialize) once the code object is ready.  Returns without waiting for the
+ * compile (only the process's first compile is preceded by the warm-up above). */
 int pcg_plan_specialize_async(pcg_plan* plan);
 
 /* SCL plans: the metric path 0 starts every frame of later decode calls with.  0 (the

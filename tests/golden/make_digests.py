@@ -35,7 +35,7 @@ CASES = {
     "config3_scl8": dict(kind="awgn", N=1024, K=512, L=8, F=1 << 16, ebn0=2.0, seed=4, crc=8),
     # tests/test_gpu_nr.py::test_decode_punctured_matches_oracle[8]: the decoder core on the
     # depunctured frames (the reference has no CRC-11: metrics, and info/ok with Dummy)
-    "config4_nr_scl8": dict(kind="nr", N=1024, K=512, L=8, F=2048, E=896, ebn0=1.25, seed=48, crc=0),
+    "config4_nr_scl8": dict(kind="nr", N=1024, K=512, L=8, F=1 << 16, E=896, ebn0=1.25, seed=48, crc=0),
     # tests/test_gpu_scl.py::test_scl32_reference_digest (config 5 code, host frames)
     "config5_scl32": dict(kind="awgn", N=4096, K=2048, L=32, F=4096, ebn0=1.5, seed=55, crc=8),
 }

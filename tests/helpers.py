@@ -24,27 +24,10 @@ LLR_KINDS = ("normal", "ints", "zeros", "sparse", "wide")
 
 
 def node_cover_sets():
-    """(N, frozen) pairs whose Fast-SSC trees contain every leaf kind at several sizes."""
-    out = []
-    # 8-bit specials
-    out.append((8, [0, 1]))                 # DoubleSpcShort8
-    out.append((8, [0, 1, 2]))              # RepRateOne8
-    out.append((8, [0, 1, 2, 3, 4]))        # ZeroSpc8
-    out.append((8, [0, 1, 2, 4]))           # TypeFive n=8
-    out.append((8, [0, 1, 2, 3, 4, 5]))     # DoubleRep n=8
-    for n in (16, 32, 64, 128):
-        out.append((n, [0, 1]))                                  # DoubleSpc
-        out.append((n, list(range(n - 3))))                      # TripleRep
-        out.append((n, sorted(set(range(n - 6)) | {n - 6, n - 4})))  # TypeFive
-        out.append((n, list(range(n - 2))))                      # DoubleRep
-        out.append((n, list(range(n // 2)) + [n // 2]))          # ZeroSpc (Q1)
-        out.append((n, list(range(n // 2 - 1))))                 # ROne at the root
-        out.append((n, list(range(n // 2)) + [n // 2, n // 2 + 1]))  # ZeroR at the root
-    # ShortRateR with n<8 leaves under it
-    out.append((8, [0, 4]))
-    out.append((8, [1, 2, 4]))
-    out.append((16, [0, 2, 8]))
-    return out
+    """(N, frozen) pairs whose Fast-SSC trees contain every leaf kind at several sizes (the
+    product's validation catalogue, antpolarcodes_amd/rtc_codes.py)."""
+    from antpolarcodes_amd.rtc_codes import node_cover_sets as f
+    return f()
 
 
 def sha256(a):
@@ -68,7 +51,7 @@ KERNELS = ("interp", "rtc")
 def gpu_plan(N, L, frozen, kernel="interp", device=0, **kw):
     """A device plan on the interpreter kernel ("interp": tests/conftest.py keeps plans from
     specialising themselves) or on its plan-specialised kernel ("rtc": pcg_plan_specialize,
-    loaded from the library's shipped cache for the test codes, antpolarcodes_amd/rtc_warm.py).
+    loaded from the library's shipped cache: the catalogue antpolarcodes_amd/rtc_codes.py).
     Asserts which kernel the decodes will launch."""
     from antpolarcodes_amd._native import Plan
     p = Plan(N, L, frozen, device=device, **kw)

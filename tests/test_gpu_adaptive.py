@@ -21,9 +21,9 @@ def _expect(oracle, N, L, fr, llr, crc, systematic=True):
 @pytest.mark.parametrize("ebn0", [1.0, 2.5])
 @pytest.mark.parametrize("crc", [8, 16, 32])
 def test_adaptive_matches_oracle(oracle, ebn0, crc, kernel):
-    """AdaptiveFloat frame by frame; "rtc": its Fast-SSC stage on the plan-specialised kernel
-    (what the library runs for the code; the list stage, a few frames per call, stays on the
-    interpreter walk)."""
+    """AdaptiveFloat frame by frame; "rtc": both stages on their plan-specialised kernels
+    (scq_rtc_kernel, then scl_rtc_kernel over the failed frames -- what the library runs for
+    the code)."""
     from antpolarcodes_amd import frames
     from helpers import gpu_plan
     N, L = 1024, 8

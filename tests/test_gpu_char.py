@@ -49,13 +49,8 @@ def _check(oracle, N, L, fr, llr, systematic=True, crc=8):
 
 
 def cover_codes():
-    out = []
-    for n in (8, 16, 32, 64, 128, 256):
-        h = n // 2
-        out += [(n, list(range(n - 1))), (n, [0]), (n, list(range(n - 2))), (n, list(range(h))),
-                (n, list(range(h)) + [h]), (n, list(range(h - 1))),
-                (n, sorted(set(list(range(h)) + [h, h + 1, h + 3]))), (n, sorted({0, 1, 2, 4, h, h + 1}))]
-    return out
+    from antpolarcodes_amd.rtc_codes import char_cover_codes
+    return char_cover_codes()
 
 
 # ------------------------------------------------------------------ FastSscFipChar
@@ -236,11 +231,9 @@ def test_adaptive_char_matches_oracle(oracle, crc, kernel):
 # ------------------------------------------------------------------ specialised FastSscFipChar
 def rtc_char_codes():
     """(N, frozen, systematic, crc) the specialised 8-bit Fast-SSC kernel is checked on (their
-    code objects ship with the library: antpolarcodes_amd/rtc_warm.py)."""
-    out = [(N, frozen_bits(N, max(8, N // 2), 0.0), True, 8) for N in (8, 32, 128, 256, 1024)]
-    out += [(64, fr, True, 0) for n, fr in cover_codes() if n == 64]
-    out += [(1024, frozen_bits(1024, 512, 0.0), sysm, crc) for sysm in (True, False) for crc in (0, 16, 32)]
-    return out
+    code objects ship with the library: antpolarcodes_amd/rtc_codes.py)."""
+    from antpolarcodes_amd.rtc_codes import char_rtc_codes
+    return char_rtc_codes()
 
 
 def test_scc_rtc_kernel(oracle):

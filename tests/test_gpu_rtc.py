@@ -114,6 +114,29 @@ def test_rtc_list_plans(oracle, N, K, L, crc, systematic, kind):
         assert np.array_equal(gm.view(np.uint32), om.view(np.uint32)), kind
 
 
+def test_rtc_list_random_frozen_sets(oracle):
+    """The specialised list kernel on random frozen sets (the catalogue's random list codes,
+    antpolarcodes_amd/rtc_codes.py: N = 32 .. 256, L = 3, 8, 32, any number of frozen
+    positions): the reference's SCL classifier (scl_avx_float.cpp:624-651) meets R0 / R1 / Rep /
+    SPC nodes and size-8 subtrees of every shape, and the layout (recomputed top stages, LDS /
+    slab split) varies with the tree.  Info, ok and ordered path metrics bit-exact against the
+    oracle, on every LLR family."""
+    from antpolarcodes_amd._native import Plan
+    from antpolarcodes_amd.rtc_codes import random_list_codes
+    rng = np.random.default_rng(404)
+    for N, L, fr in random_list_codes():
+        p = Plan(N, L, fr, crc=0, device=0)
+        p.specialize()
+        assert p.describe()["specialized"] == 1 and p.kernel_name() == "scl_rtc_kernel"
+        for kind in LLR_KINDS:
+            llr = llr_kinds(rng, 64, N, kind)
+            gi, gok, gm = p.decode_host(llr, want_metrics=True)
+            oi, ook, om, _, _ = oracle.scl_decode(N, L, fr, llr, crc=0, paths=True)
+            assert np.array_equal(gi, oi), (N, L, len(fr), kind)
+            assert np.array_equal(gok, ook), (N, L, len(fr), kind)
+            assert np.array_equal(gm.view(np.uint32), om.view(np.uint32)), (N, L, len(fr), kind)
+
+
 def test_rtc_default_mode_list_plan(oracle, monkeypatch):
     """The library default (PCG_RTC=2) on list plans: a code whose specialised kernel is in the
     shipped cache (config 3) runs it from its first decode; a code that is not (N=1024 K=600

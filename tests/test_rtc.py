@@ -125,17 +125,30 @@ def test_destroy_during_compile_and_shared_compile(tmp_path):
     assert len(list((tmp_path / "b").glob("pcg_*.co"))) == 1
 
 
-def test_shipped_cache_holds_the_benchmark_codes():
-    """The build (antpolarcodes_amd/rtc_warm.py) ships the specialised kernels of the benchmark
-    configurations next to the library: they load without any compile."""
-    code = ("from antpolarcodes_amd.rtc_warm import bench_codes\n"
-            "for N, L, (kind, K), crc, sysm, *ad in bench_codes():\n"
-            "    p = Plan(N, L, frozen_bits(N, K, 0.0, kind), systematic=sysm, crc=crc, device=-1,\n"
-            "             adaptive=ad[:1] in (['adaptive'], ['adaptive_char']),\n"
-            "             fixed=ad[:1] in (['char'], ['adaptive_char']))\n"
+def test_shipped_cache_holds_the_catalogue():
+    """The build (antpolarcodes_amd/rtc_warm.py) ships the specialised kernels of the whole
+    catalogue (antpolarcodes_amd/rtc_codes.py: the benchmark configurations and the validation
+    codes the GPU tests use) next to the library, with the hiprtc version they were built by:
+    they load without any compile."""
+    import os
+    from antpolarcodes_amd import rtc_warm
+    assert os.path.isfile(os.path.join(rtc_warm.CACHE, "HIPRTC_VERSION"))
+    code = ("from antpolarcodes_amd.rtc_codes import codes\n"
+            "from antpolarcodes_amd._native import PcgError\n"
+            "n = 0\n"
+            "for N, L, (kind, arg), crc, sysm, *ad in codes():\n"
+            "    fr = list(arg) if kind == 'set' else frozen_bits(N, arg, 0.0, kind)\n"
+            "    try:\n"
+            "        p = Plan(N, L, fr, systematic=sysm, crc=crc, device=-1,\n"
+            "                 adaptive=ad[:1] in (['adaptive'], ['adaptive_char']),\n"
+            "                 fixed=ad[:1] in (['char'], ['adaptive_char']))\n"
+            "    except PcgError:\n"
+            "        continue\n"
             "    p.specialize()\n"
-            "print('compiles', lib().pcg_dev_rtc_compiles())\n")
-    assert "compiles 0" in _run(code, {"PCG_RTC_CACHE": "0"}, timeout=120)
+            "    n += 1\n"
+            "print('codes', n, 'compiles', lib().pcg_dev_rtc_compiles())\n")
+    out = _run(code, {"PCG_RTC_CACHE": "0"}, timeout=300)
+    assert "compiles 0" in out, out
 
 
 def test_dev_build_knobs_reach_the_specialised_source():
