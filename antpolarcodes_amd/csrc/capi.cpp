@@ -7,6 +7,7 @@
 #include "rtc.hpp"
 
 #include <hip/hip_runtime.h>
+#include <emmintrin.h>
 
 #include <algorithm>
 #include <cstring>
@@ -1084,8 +1085,8 @@ int pcg_decode_i8(pcg_plan* p,
 //   0  serial: blocking pageable copies, then the decode, chunk by chunk (no overlap);
 //   1  the caller's pageable buffer copied by the runtime on the copy stream (the host thread
 //      blocks in the copy while the previous chunk decodes);
-//   2  plan-owned pinned staging filled by PCG_HOST_THREADS host threads (default 8), then a
-//      DMA copy on the copy stream.
+//   2  plan-owned pinned staging filled by PCG_HOST_THREADS host threads (default 8; with
+//      non-temporal stores, PCG_HOST_NT=0: plain memcpy), then a DMA copy on the copy stream.
 // A caller buffer that is already pinned (hipHostMalloc / hipHostRegister) is copied from
 // directly in modes 1 and 2.  PCG_HOST_CHUNK overrides the chunk size in frames (default:
 // 64 MB of input, between 4096 and 65536 frames).
@@ -1095,12 +1096,40 @@ static int env_int(const char* name, int dflt)
     return e && *e ? atoi(e) : dflt;
 }
 
-static void par_memcpy(void* dst, const void* src, size_t bytes, int threads)
+// A copy into the pinned staging with non-temporal 16-byte stores: the destination is only read
+// by the DMA engine, so its lines need not be fetched into the cache first (ordinary stores read
+// each line before writing it: a third of the host memory traffic of the staging copy).
+static void nt_memcpy(void* dst, const void* src, size_t bytes)
 {
+    char* d = (char*)dst;
+    const char* s = (const char*)src;
+    size_t head = (16 - ((uintptr_t)d & 15)) & 15;
+    if (head > bytes)
+        head = bytes;
+    memcpy(d, s, head);
+    d += head;
+    s += head;
+    bytes -= head;
+    size_t i = 0;
+    for (; i + 64 <= bytes; i += 64) {
+        const __m128i a = _mm_loadu_si128((const __m128i*)(s + i)), b = _mm_loadu_si128((const __m128i*)(s + i + 16)),
+                      c = _mm_loadu_si128((const __m128i*)(s + i + 32)), e = _mm_loadu_si128((const __m128i*)(s + i + 48));
+        _mm_stream_si128((__m128i*)(d + i), a);
+        _mm_stream_si128((__m128i*)(d + i + 16), b);
+        _mm_stream_si128((__m128i*)(d + i + 32), c);
+        _mm_stream_si128((__m128i*)(d + i + 48), e);
+    }
+    memcpy(d + i, s + i, bytes - i);
+    _mm_sfence();
+}
+
+static void par_memcpy(void* dst, const void* src, size_t bytes, int threads, bool nt)
+{
+    auto cp = nt ? nt_memcpy : [](void* d, const void* s, size_t n) { memcpy(d, s, n); };
     const size_t per = size_t(4) << 20; // at least 4 MB per thread
     int t = (int)std::min<size_t>((size_t)std::max(threads, 1), (bytes + per - 1) / per);
     if (t <= 1) {
-        memcpy(dst, src, bytes);
+        cp(dst, src, bytes);
         return;
     }
     const size_t part = ((bytes + t - 1) / t + 4095) & ~size_t(4095);
@@ -1109,9 +1138,9 @@ static void par_memcpy(void* dst, const void* src, size_t bytes, int threads)
         const size_t o = part * k;
         if (o >= bytes)
             break;
-        th.emplace_back([=] { memcpy((char*)dst + o, (const char*)src + o, std::min(part, bytes - o)); });
+        th.emplace_back([=] { cp((char*)dst + o, (const char*)src + o, std::min(part, bytes - o)); });
     }
-    memcpy(dst, src, std::min(part, bytes));
+    cp(dst, src, std::min(part, bytes));
     for (auto& x : th)
         x.join();
 }
@@ -1217,6 +1246,7 @@ static int decode_host(pcg_plan* p, const void* llr, size_t elem, uint64_t F, ui
     const bool direct = host_pinned(llr);
     const bool stage = mode == 2 && !direct;
     const int threads = env_int("PCG_HOST_THREADS", 8);
+    const bool nt = env_int("PCG_HOST_NT", 1) != 0;
     int rc = pipe_alloc(p, chunk, fb, stage);
     if (rc != 0)
         return rc;
@@ -1254,7 +1284,7 @@ static int decode_host(pcg_plan* p, const void* llr, size_t elem, uint64_t F, ui
             return rc;
         const char* src = (const char*)llr + f0 * fb;
         if (stage) {
-            par_memcpy(q->h_in[b], src, n * fb, threads);
+            par_memcpy(q->h_in[b], src, n * fb, threads, nt);
             src = (const char*)q->h_in[b];
         }
         if ((e = hipMemcpyAsync(q->d_in[b], src, n * fb, hipMemcpyHostToDevice, q->copy)) != hipSuccess)

@@ -588,6 +588,11 @@ PCG_DEV void ls_fg(Src src, Dst dst, const DBits& lb, uint32_t s, const Share& w
 template <int OPC, bool FU, int LP>
 PCG_DEV void ls_rootv_op(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, uint32_t s, uint32_t o, const Share& w,
                          uint32_t m);
+// Recomputed quarters / eighths of a codeword with P < LP paths: the idle lanes share the
+// path's staged rounds (at most as many lanes per path as a round has output chunks)
+#ifndef PCG_DEEP_SHARE
+#define PCG_DEEP_SHARE 1
+#endif
 template <int LP>
 PCG_DEV uint32_t ls_root_round(const Ls<LP>& c, uint32_t s, uint32_t h, bool fused);
 
@@ -598,7 +603,8 @@ PCG_DEV void ls_fg_op(Ls<LP>& c, uint32_t s, uint32_t o, uint32_t P)
     if (d >= c.mt || d < 3u + c.vlow) // recomputed where it is read
         return;
     const bool deep = s >= c.mt && s + 2u <= c.top; // a recomputed quarter / eighth
-    const Share w = ls_share(c, P, s, deep ? 0u : 1u << (s - 3)); // (those: one lane per path)
+    // (those: at most as many lanes per path as one staging round has output chunks)
+    const Share w = ls_share(c, P, s, deep ? PCG_DEEP_SHARE * 2u * ls_root_round(c, s, 1u, false) : 1u << (s - 3));
     const DBits lb = gbits(c, s, o, w.dl, w.bl);
     if (deep) { // its child is a leaf: staged, unfused (alpha[s-1] is global)
         const uint32_t rm = ls_root_round(c, s, w.h, false);
@@ -838,6 +844,46 @@ PCG_DEV uint32_t ls_root_round(const Ls<LP>& c, uint32_t s, uint32_t h, bool fus
 // the bits of the left child of the level-l ancestor -- vb[l-1]: the root's left half, then
 // D[top-1] / the row at that node, D[top-2] / ...  FU = false: the X alone (its child is a
 // leaf): output chunk c2 < hq of alpha[s-1] from alpha[s] chunks c2, c2+hq.
+// Double-buffered rounds (PCG_STG_DB): the staging region is split in two halves of m/2 output
+// chunks each; round k+1's DMA is issued into one half before round k computes from the other,
+// and the wave waits for all but that round's DMA instructions (s_waitcnt vmcnt(ninst)) -- so a
+// round's fetch latency overlaps the previous round's arithmetic instead of adding to it.
+#ifndef PCG_STG_DB
+#define PCG_STG_DB 1
+#endif
+// s_waitcnt: vector memory counter <= n (loads, stores and LDS DMA, in issue order), the others
+// not waited for (gfx9 encoding: vmcnt [3:0] and [15:14], expcnt [6:4], lgkmcnt [11:8])
+#define PCG_WAIT_VM(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | ((((n) >> 4) & 3) << 14) | (7 << 4) | (15 << 8))
+// One LDS-DMA instruction (16 B per lane, lane-linear 1 KiB at lds), written as inline asm: the
+// compiler's own wait bookkeeping does not see it, so it does not drain it (vmcnt(0)) before
+// every LDS read of the other half -- the double-buffered rounds count it themselves (wait_vm,
+// then a barrier, then the reads).  M0 is set and restored in the same statement
+// (cdna_hip_programming.md, LDS-DMA recipe).
+PCG_DEV void glds16(const float* src, float* lds)
+{
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds);
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(dst)
+                 : "memory");
+}
+PCG_DEV void wait_vm(uint32_t n) // (wave-uniform n; the instruction takes an immediate)
+{
+    switch (n) {
+    case 1: PCG_WAIT_VM(1); break;
+    case 2: PCG_WAIT_VM(2); break;
+    case 3: PCG_WAIT_VM(3); break;
+    case 4: PCG_WAIT_VM(4); break;
+    case 6: PCG_WAIT_VM(6); break;
+    case 8: PCG_WAIT_VM(8); break;
+    case 12: PCG_WAIT_VM(12); break;
+    case 16: PCG_WAIT_VM(16); break;
+    default: __builtin_amdgcn_s_waitcnt(0); break; // (any other count: wait for all)
+    }
+}
+
 template <int OPC, int V, int RM, bool FU, int LP>
 PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, const DBits (&vb)[3], uint32_t s,
                           const Share& w, uint32_t m)
@@ -847,8 +893,16 @@ PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, co
     const uint32_t hl[3] = { c.N >> 3, c.N >> 4, c.N >> 5 };
     const uint32_t nout = FU ? hq2 : hq;           // output chunks of the op
     float* stg = c.lds + c.ly.alpha;
+    // (wave-uniform) two half-size buffers when each half still gives every lane an output chunk --
+    // with codeword rows only: with D buffers (LP >= 16) the level bits are global loads that the
+    // compiler waits for with vmcnt(0), which drains the next round's DMA as well (measured, config
+    // 5: 1.244e6 -> 1.203e6 cw/s; config 3, rows: 2.844e7 -> 2.874e7; profiles/r05b_*)
+    const bool dbl = PCG_STG_DB && !Ls<LP>::DB && (m >> 1) >= w.h && (64u / LP) * KS * J * (m >> 1) >= 64u;
+    if (dbl)
+        m >>= 1;
     const uint32_t per = KS * J * m;               // chunks per codeword per round
     const uint32_t ninst = (64u / LP) * per / 64u; // DMA instructions per round
+    const uint32_t hoff = dbl ? ninst * 256u : 0u; // floats: the second half
     const uint32_t n = m / w.h;                    // output chunks per lane per round
     const uint64_t yp = (uint64_t)(uintptr_t)c.y;
     const float4* stg4 = reinterpret_cast<const float4*>(stg);
@@ -886,9 +940,8 @@ PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, co
                 lw[1] = lb.wat(4u * (cg + hq2));
         }
     };
-    for (uint32_t r = 0; r < nout; r += m) {
-        __builtin_amdgcn_s_waitcnt(0); // the previous round's LDS reads have completed
-        __builtin_amdgcn_wave_barrier();
+    // round r's channel chunks into the half at float offset hb
+    auto issue = [&](uint32_t r, uint32_t hb) {
         for (uint32_t t = 0; t < ninst; ++t) {
             const uint32_t f = t * 64u + c.lane;
             uint32_t g, rem;
@@ -900,14 +953,39 @@ PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, co
                 a += ((j >> (l - 1)) & 1u) ? hl[l - 1] : 0u;
             const uint32_t lo = shfl((uint32_t)yp, (int)(g * LP)), hi = shfl((uint32_t)(yp >> 32), (int)(g * LP));
             const float* src = reinterpret_cast<const float*>((uintptr_t)(((uint64_t)hi << 32) | lo)) + 4u * a;
-            __builtin_amdgcn_global_load_lds(src, stg + t * 256u, 16, 0, 0);
+            if (PCG_STG_DB && !Ls<LP>::DB) // (every round explicitly waited for: s_waitcnt / wait_vm below)
+                glds16(src, stg + hb + t * 256u);
+            else
+                __builtin_amdgcn_global_load_lds(src, stg + hb + t * 256u, 16, 0, 0);
+        }
+    };
+    if (dbl) {
+        __builtin_amdgcn_s_waitcnt(0); // (the region's previous readers have completed)
+        __builtin_amdgcn_wave_barrier();
+        issue(0, 0);
+    }
+    uint32_t hb = 0;
+    for (uint32_t r = 0; r < nout; r += m, hb ^= hoff) {
+        if (!dbl) {
+            __builtin_amdgcn_s_waitcnt(0); // the previous round's LDS reads have completed
+            __builtin_amdgcn_wave_barrier();
+            issue(r, 0);
         }
         if (w.act)
             words(r + w.i * n);
-        __builtin_amdgcn_s_waitcnt(0);
+        if (dbl && r + m < nout) {
+            // the other half's readers (the previous round) have completed: fetch the next round
+            // into it, then wait for everything but those DMA instructions
+            __builtin_amdgcn_wave_barrier();
+            issue(r + m, hb ^ hoff);
+            wait_vm(ninst);
+        } else {
+            __builtin_amdgcn_s_waitcnt(0);
+        }
         __builtin_amdgcn_wave_barrier();
         if (!w.act)
             continue;
+        const float4* cur = stg4 + (hb >> 2);
         for (uint32_t uu = 0; uu < n; ++uu) {
             const uint32_t u = w.i * n + uu, c2 = r + u;
             if (uu > 0 && (uu & 7u) == 0)
@@ -919,7 +997,7 @@ PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, co
                 float4 v[J];
 #pragma unroll
                 for (uint32_t j = 0; j < J; ++j)
-                    v[j] = stg4[stg_idx<LP>((u * KS + k) * J + j, mg, per)];
+                    v[j] = cur[stg_idx<LP>((u * KS + k) * J + j, mg, per)];
 #pragma unroll
                 for (int l = 1; l <= V; ++l)
 #pragma unroll
@@ -996,7 +1074,9 @@ PCG_DEV void ls_fgf_op(Ls<LP>& c, uint32_t s, uint32_t o, uint32_t P)
 {
     const uint32_t d = s - 1, e = s - 2;
     const bool rootc = s >= c.mt && s != c.top, left = o < (c.N >> 1), deep = rootc && s + 2u <= c.top;
-    const Share w = ls_share(c, P, s, deep ? 0u : 1u << (s - 4)); // (quarters / eighths: one lane per path)
+    // (quarters / eighths: at most as many lanes per path as a staging round has output chunks,
+    // so that the idle lanes of a codeword with P < LP paths share its staged rounds)
+    const Share w = ls_share(c, P, s, deep ? PCG_DEEP_SHARE * 2u * ls_root_round(c, s, 1u, true) : 1u << (s - 4));
     const DBits lb = gbits(c, s, o, w.dl, w.bl);
     const uint32_t rm = ls_root_round(c, s, w.h, true);
     if (deep) { // a recomputed quarter / eighth: staged (its grandchild alpha[s-2] is global)
@@ -2868,6 +2948,8 @@ std::string sclls_rtc_defines(bool* nondefault)
     d("PCG_LS_DBITS_LP", PCG_LS_DBITS_LP, 16);
     d("PCG_FGF_U", PCG_FGF_U, 1);
     d("PCG_STG_GM", PCG_STG_GM, 1);
+    d("PCG_STG_DB", PCG_STG_DB, 1);
+    d("PCG_DEEP_SHARE", PCG_DEEP_SHARE, 1);
     d("PCG_SEL_BITONIC_LP", PCG_SEL_BITONIC_LP, 16);
     d("PCG_SEL_BITONIC_K", PCG_SEL_BITONIC_K, 4);
     d("PCG_SEL_VMERGE", PCG_SEL_VMERGE, 0);

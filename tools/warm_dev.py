@@ -2,7 +2,7 @@
 (PCG_DEV_LIB variant, layout knobs such as PCG_SCL_LDS_KB) into a dev cache directory, so an
 A/B sweep on the GPU box loads it instead of compiling there (development aid).
     PCG_DEV_LIB=lib_dev/libpcg_x.so [PCG_...] python tools/warm_dev.py <cache dir> <mode> ...
-modes: the bench_codes() entries of antpolarcodes_amd/rtc_warm.py by bench mode name.
+modes: the bench_codes() entries of antpolarcodes_amd/rtc_codes.py by bench mode name.
 On the box: PCG_RTC_CACHE=<cache dir> with the same PCG_* settings."""
 import os
 import subprocess
@@ -10,7 +10,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from antpolarcodes_amd.rtc_warm import bench_codes  # noqa: E402
+from antpolarcodes_amd.rtc_codes import bench_codes  # noqa: E402
 
 MODES = dict(zip(["sc", "scl8", "adaptive8", "nr5g", "scl32", "sc_char", "scl8_char", "adaptive8_char"],
                  bench_codes()))
