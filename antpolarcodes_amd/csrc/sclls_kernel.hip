@@ -1219,9 +1219,22 @@ PCG_DEV void ls_comb(Ls<LP>& c, uint32_t s, uint32_t o, bool act)
         if (!act)
             return;
         if (h >= 32) {
+            // (the left words are written, the right ones only read: 8 word pairs loaded per
+            // batch before their stores, not one dependent LDS round trip per word)
             const uint32_t wl = o >> 5, wr = (o + h) >> 5, nw = h >> 5;
-            for (uint32_t w = 0; w < nw; ++w)
-                row[(wl + w) << 6] ^= row[(wr + w) << 6];
+            for (uint32_t w = 0; w < nw; w += 8) {
+                uint32_t l[8], r[8];
+#pragma unroll
+                for (uint32_t u = 0; u < 8; ++u)
+                    if (w + u < nw) {
+                        l[u] = row[(wl + w + u) << 6];
+                        r[u] = row[(wr + w + u) << 6];
+                    }
+#pragma unroll
+                for (uint32_t u = 0; u < 8; ++u)
+                    if (w + u < nw)
+                        row[(wl + w + u) << 6] = l[u] ^ r[u];
+            }
         } else {
             const uint32_t sh = o & 31u, msk = ((1u << h) - 1u) << sh;
             lds_u32* w = row + ((o >> 5) << 6);
@@ -1889,12 +1902,91 @@ constexpr uint32_t k32_cb()
 {
     return LP <= 2 ? 4u : LP <= 4 ? 5u : LP <= 8 ? 6u : LP <= 16 ? 7u : 8u;
 }
+// Top-8 of an 8-lane group's 64 keys (LP = 8, K = 8: SPC leaves, np <= 8): instead of sorting
+// all 64, three butterfly levels each merge the lane's sorted 8 with its partner's into the top
+// 8 of both (max against the partner's run reversed: a bitonic sequence, then three in-register
+// half-cleaners), after which every lane of the group holds the group's sorted top 8 -- 3 x 20
+// compare-exchanges instead of the full bitonic sort's 84, and each survivor reads its key from
+// its own registers (no cross-lane extraction).  The first non-survivor (R = np + 1 = 9, for the
+// tie test) is the group maximum of the keys below the 8th.  Same keys, same order: the result
+// and the near-tie test are the full sort's.
+#ifndef PCG_SEL_TOP8
+#define PCG_SEL_TOP8 1
+#endif
+template <int D>
+PCG_DEV void top8_level(uint32_t (&q)[8])
+{
+    uint32_t t[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        t[j] = bfly<D>(q[7 - j]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        q[j] = umax32(q[j], t[j]);
+    bit_regs32<8, 4>(q);
+}
+template <int LP>
+PCG_DEV bool k32_top8(const Ls<LP>& c, const float (&cv)[8], uint32_t P, uint32_t np, uint32_t R, float& val,
+                      uint32_t& src, uint32_t& jsel)
+{
+    constexpr uint32_t CB = k32_cb<LP>(), cm = (1u << CB) - 1u;
+    const bool act = c.p < P;
+    auto key = [&](int j) { return act ? ((ordz(cv[j]) & ~cm) | (~((c.p << 3) | (uint32_t)j) & cm)) : 0u; };
+    uint32_t q[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        q[j] = key(j);
+    local_order32<8>(q);
+    top8_level<1>(q);
+    top8_level<2>(q);
+    top8_level<4>(q);
+    // near ties among the first R (<= 9) of the group's sequence: q[0..7], then the 9th
+    bool near = false;
+#pragma unroll
+    for (int j = 0; j + 1 < 8; ++j)
+        if ((uint32_t)j + 1u < R)
+            near = near | ((q[j] >> CB) == (q[j + 1] >> CB));
+    if (R > 8u) {
+        uint32_t m9 = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t k = key(j);
+            m9 = umax32(m9, k < q[7] ? k : 0u);
+        }
+        m9 = umax32(m9, bfly<1>(m9));
+        m9 = umax32(m9, bfly<2>(m9));
+        m9 = umax32(m9, bfly<4>(m9));
+        near = near | ((q[7] >> CB) == (m9 >> CB));
+    }
+    if (ballot(near) != 0ull)
+        return false;
+    uint32_t mk = q[0];
+#pragma unroll
+    for (int j = 1; j < 8; ++j)
+        mk = c.p == (uint32_t)j ? q[j] : mk;
+    const uint32_t code = ~mk & cm;
+    src = code >> 3;
+    jsel = code & 7u;
+    float vv = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float x = shfl(cv[j], (int)(c.gb | src));
+        if ((uint32_t)j == jsel)
+            vv = x;
+    }
+    val = vv;
+    (void)np;
+    return true;
+}
+
 // Selection on 32-bit keys: true and (val, src, jsel) when no group has a near tie among its
 // first R selected keys, else false (the caller runs the exact sort).
 template <int LP, int K>
 PCG_DEV bool k32_select(const Ls<LP>& c, const float (&cv)[8], uint32_t P, uint32_t np, uint32_t R, float& val,
                         uint32_t& src, uint32_t& jsel)
 {
+    if constexpr (PCG_SEL_TOP8 && LP == 8 && K == 8)
+        return k32_top8<LP>(c, cv, P, np, R, val, src, jsel);
     constexpr uint32_t CB = k32_cb<LP>(), cm = (1u << CB) - 1u;
     const bool act = c.p < P;
     uint32_t q[8];
@@ -2950,6 +3042,8 @@ std::string sclls_rtc_defines(bool* nondefault)
     d("PCG_STG_GM", PCG_STG_GM, 1);
     d("PCG_STG_DB", PCG_STG_DB, 1);
     d("PCG_DEEP_SHARE", PCG_DEEP_SHARE, 1);
+    d("PCG_F_OLD", PCG_F_OLD, 0);
+    d("PCG_SEL_TOP8", PCG_SEL_TOP8, 1);
     d("PCG_SEL_BITONIC_LP", PCG_SEL_BITONIC_LP, 16);
     d("PCG_SEL_BITONIC_K", PCG_SEL_BITONIC_K, 4);
     d("PCG_SEL_VMERGE", PCG_SEL_VMERGE, 0);

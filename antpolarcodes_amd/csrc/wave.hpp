@@ -39,12 +39,25 @@ PCG_DEV float minps(float a, float b) { return a < b ? a : b; }
 PCG_DEV float maxps(float a, float b) { return a > b ? a : b; }
 
 // f: sign(a)^sign(b) | min(|a|,|b|)          avx_float.h:55-63
-// (float |.| so the compare and the select take abs source modifiers: v_cmp_lt |a|,|b|;
-// v_cndmask |b|,|a|; v_xor; v_and_or -- MINPS semantics, the second operand on ties and NaN)
+// MINPS semantics (the second operand on ties and NaN): the compare takes abs source modifiers
+// and the select picks the SIGNED operand whose magnitude wins, so the sign merge is one bit
+// select -- v_cmp_lt |a|,|b|; v_cndmask; v_xor; v_bfi (4 VALU; selecting |a| / |b| instead
+// made the compiler add a v_and per element: 5)
+#ifndef PCG_F_OLD
+#define PCG_F_OLD 0 // dev A/B: 1 = the round-4 formulation (abs values selected: 5 VALU)
+#endif
 PCG_DEV float polar_f(float a, float b)
 {
+#if PCG_F_OLD
     const float aa = __builtin_fabsf(a), ab = __builtin_fabsf(b);
     return ubits(((fbits(a) ^ fbits(b)) & 0x80000000u) | fbits(aa < ab ? aa : ab));
+#endif
+    const uint32_t ua = fbits(a), ub = fbits(b);
+    const uint32_t sel = __builtin_fabsf(a) < __builtin_fabsf(b) ? ua : ub;
+    // S2 ? S0 : S1 with S2 = the sign mask: the sign of a ^ b, the rest of sel (truth table
+    // 0xE4: bit i = f(S0 = i>>2 & 1, S1 = i>>1 & 1, S2 = i & 1), the convention of 0x78 below)
+    // (written as the builtin: the compiler turns the plain expression back into and + and_or)
+    return ubits(__builtin_amdgcn_bitop3_b32(ua ^ ub, sel, 0x80000000u, 0xE4));
 }
 // g: (a ^ signbit) + b                       avx_float.h:71-81
 PCG_DEV float polar_g(float a, float b, uint32_t signbit) { return fxor(a, signbit) + b; }
