@@ -851,6 +851,12 @@ PCG_DEV uint32_t ls_root_round(const Ls<LP>& c, uint32_t s, uint32_t h, bool fus
 #ifndef PCG_STG_DB
 #define PCG_STG_DB 1
 #endif
+#ifndef PCG_STG_TAIL_DRAIN
+#define PCG_STG_TAIL_DRAIN 0 // 1: the recomputed-node ops end waiting for their stores too
+#endif
+#ifndef PCG_STG_RING
+#define PCG_STG_RING 2 // at most this many buffers (measured: 3 buffers -1 % against 2 on config 3, r05g)
+#endif
 // s_waitcnt: vector memory counter <= n (loads, stores and LDS DMA, in issue order), the others
 // not waited for (gfx9 encoding: vmcnt [3:0] and [15:14], expcnt [6:4], lgkmcnt [11:8])
 #define PCG_WAIT_VM(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | ((((n) >> 4) & 3) << 14) | (7 << 4) | (15 << 8))
@@ -869,19 +875,92 @@ PCG_DEV void glds16(const float* src, float* lds)
                  : "v"(src), "s"(dst)
                  : "memory");
 }
-PCG_DEV void wait_vm(uint32_t n) // (wave-uniform n; the instruction takes an immediate)
+PCG_DEV void wait_vm(uint32_t n) // (wave-uniform n <= 63; the instruction takes an immediate)
 {
     switch (n) {
     case 1: PCG_WAIT_VM(1); break;
     case 2: PCG_WAIT_VM(2); break;
     case 3: PCG_WAIT_VM(3); break;
     case 4: PCG_WAIT_VM(4); break;
+    case 5: PCG_WAIT_VM(5); break;
     case 6: PCG_WAIT_VM(6); break;
+    case 7: PCG_WAIT_VM(7); break;
     case 8: PCG_WAIT_VM(8); break;
+    case 9: PCG_WAIT_VM(9); break;
+    case 10: PCG_WAIT_VM(10); break;
+    case 11: PCG_WAIT_VM(11); break;
     case 12: PCG_WAIT_VM(12); break;
+    case 13: PCG_WAIT_VM(13); break;
+    case 14: PCG_WAIT_VM(14); break;
+    case 15: PCG_WAIT_VM(15); break;
     case 16: PCG_WAIT_VM(16); break;
-    default: __builtin_amdgcn_s_waitcnt(0); break; // (any other count: wait for all)
+    case 17: PCG_WAIT_VM(17); break;
+    case 18: PCG_WAIT_VM(18); break;
+    case 19: PCG_WAIT_VM(19); break;
+    case 20: PCG_WAIT_VM(20); break;
+    case 21: PCG_WAIT_VM(21); break;
+    case 22: PCG_WAIT_VM(22); break;
+    case 23: PCG_WAIT_VM(23); break;
+    case 24: PCG_WAIT_VM(24); break;
+    case 25: PCG_WAIT_VM(25); break;
+    case 26: PCG_WAIT_VM(26); break;
+    case 27: PCG_WAIT_VM(27); break;
+    case 28: PCG_WAIT_VM(28); break;
+    case 29: PCG_WAIT_VM(29); break;
+    case 30: PCG_WAIT_VM(30); break;
+    case 31: PCG_WAIT_VM(31); break;
+    case 32: PCG_WAIT_VM(32); break;
+    case 33: PCG_WAIT_VM(33); break;
+    case 34: PCG_WAIT_VM(34); break;
+    case 35: PCG_WAIT_VM(35); break;
+    case 36: PCG_WAIT_VM(36); break;
+    case 37: PCG_WAIT_VM(37); break;
+    case 38: PCG_WAIT_VM(38); break;
+    case 39: PCG_WAIT_VM(39); break;
+    case 40: PCG_WAIT_VM(40); break;
+    case 41: PCG_WAIT_VM(41); break;
+    case 42: PCG_WAIT_VM(42); break;
+    case 43: PCG_WAIT_VM(43); break;
+    case 44: PCG_WAIT_VM(44); break;
+    case 45: PCG_WAIT_VM(45); break;
+    case 46: PCG_WAIT_VM(46); break;
+    case 47: PCG_WAIT_VM(47); break;
+    case 48: PCG_WAIT_VM(48); break;
+    case 49: PCG_WAIT_VM(49); break;
+    case 50: PCG_WAIT_VM(50); break;
+    case 51: PCG_WAIT_VM(51); break;
+    case 52: PCG_WAIT_VM(52); break;
+    case 53: PCG_WAIT_VM(53); break;
+    case 54: PCG_WAIT_VM(54); break;
+    case 55: PCG_WAIT_VM(55); break;
+    case 56: PCG_WAIT_VM(56); break;
+    case 57: PCG_WAIT_VM(57); break;
+    case 58: PCG_WAIT_VM(58); break;
+    case 59: PCG_WAIT_VM(59); break;
+    case 60: PCG_WAIT_VM(60); break;
+    case 61: PCG_WAIT_VM(61); break;
+    case 62: PCG_WAIT_VM(62); break;
+    case 63: PCG_WAIT_VM(63); break;
+    default: __builtin_amdgcn_s_waitcnt(0); break; // (0, or any larger count: wait for all)
     }
+}
+
+// The leading recompute levels whose combine is F (RM's low zero bits) do not depend on the path:
+// they are computed once per codeword, by the whole wave right after a round lands (any lane,
+// any codeword: the staged groups are spread over the 64 lanes), in place in the staged image --
+// so every path reads J >> L0 chunks per source instead of J and skips those levels.  (Config 3:
+// the codeword's first two quarters, whose level 1 is F(y_j, y_j+N/2); the first quarter's
+// level 2 too.)
+#ifndef PCG_STG_SHARED_F
+#define PCG_STG_SHARED_F 1
+#endif
+template <int V, int RM>
+constexpr uint32_t rm_lead_f()
+{
+    uint32_t l = 0;
+    while (PCG_STG_SHARED_F && l < (uint32_t)V && !((RM >> l) & 1))
+        ++l;
+    return l;
 }
 
 template <int OPC, int V, int RM, bool FU, int LP>
@@ -889,20 +968,29 @@ PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, co
                           const Share& w, uint32_t m)
 {
     constexpr uint32_t KS = FU ? 4u : 2u, J = 1u << V;
+    constexpr uint32_t L0 = rm_lead_f<V, RM>(), J0 = J >> L0; // shared levels, chunks left per source
     const uint32_t hq = 1u << (s - 3), hq2 = hq >> 1;
     const uint32_t hl[3] = { c.N >> 3, c.N >> 4, c.N >> 5 };
     const uint32_t nout = FU ? hq2 : hq;           // output chunks of the op
     float* stg = c.lds + c.ly.alpha;
-    // (wave-uniform) two half-size buffers when each half still gives every lane an output chunk --
-    // with codeword rows only: with D buffers (LP >= 16) the level bits are global loads that the
-    // compiler waits for with vmcnt(0), which drains the next round's DMA as well (measured, config
-    // 5: 1.244e6 -> 1.203e6 cw/s; config 3, rows: 2.844e7 -> 2.874e7; profiles/r05b_*)
+    // (wave-uniform) a ring of NB buffers of m/2 output chunks each -- as many as the LDS stage
+    // region holds, at most 4 -- when a buffer still gives every lane an output chunk: NB-1 rounds'
+    // fetches stay in flight while one computes (the ops are bound by the fetch latency: 32 KB of
+    // channel per wave and op through a 12 KB region, config 3).  With codeword rows only: with D
+    // buffers (LP >= 16) the level bits are global loads that the compiler waits for with vmcnt(0),
+    // which drains the in-flight rounds as well (measured with two buffers, config 5: 1.244e6 ->
+    // 1.203e6 cw/s; config 3, rows: 2.844e7 -> 2.874e7; profiles/r05b_*)
     const bool dbl = PCG_STG_DB && !Ls<LP>::DB && (m >> 1) >= w.h && (64u / LP) * KS * J * (m >> 1) >= 64u;
-    if (dbl)
+    uint32_t NB = 1;
+    if (dbl) {
         m >>= 1;
+        const uint32_t region = 4u * 64u * ((1u << c.Sl) - c.ab);    // bytes
+        NB = region / ((64u / LP) * KS * J * m * 16u);
+        NB = NB > (uint32_t)PCG_STG_RING ? (uint32_t)PCG_STG_RING : NB;
+    }
     const uint32_t per = KS * J * m;               // chunks per codeword per round
     const uint32_t ninst = (64u / LP) * per / 64u; // DMA instructions per round
-    const uint32_t hoff = dbl ? ninst * 256u : 0u; // floats: the second half
+    const uint32_t hoff = dbl ? ninst * 256u : 0u; // floats: one buffer
     const uint32_t n = m / w.h;                    // output chunks per lane per round
     const uint64_t yp = (uint64_t)(uintptr_t)c.y;
     const float4* stg4 = reinterpret_cast<const float4*>(stg);
@@ -942,6 +1030,9 @@ PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, co
     };
     // round r's channel chunks into the half at float offset hb
     auto issue = [&](uint32_t r, uint32_t hb) {
+#if defined(PCG_DEV_ABL_DEEP) && PCG_DEV_ABL_DEEP == 1 // dev ablation (wrong results): no channel DMA
+        return;
+#endif
         for (uint32_t t = 0; t < ninst; ++t) {
             const uint32_t f = t * 64u + c.lane;
             uint32_t g, rem;
@@ -959,13 +1050,16 @@ PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, co
                 __builtin_amdgcn_global_load_lds(src, stg + hb + t * 256u, 16, 0, 0);
         }
     };
+    // round k lives in buffer k % NB; the first NB-1 rounds are fetched up front
+    const uint32_t R = (nout + m - 1) / m;
     if (dbl) {
         __builtin_amdgcn_s_waitcnt(0); // (the region's previous readers have completed)
         __builtin_amdgcn_wave_barrier();
-        issue(0, 0);
+        for (uint32_t k = 0; k + 1 < NB && k < R; ++k)
+            issue(k * m, k * hoff);
     }
-    uint32_t hb = 0;
-    for (uint32_t r = 0; r < nout; r += m, hb ^= hoff) {
+    uint32_t hb = 0, kb = 0;
+    for (uint32_t r = 0, k = 0; r < nout; r += m, ++k) {
         if (!dbl) {
             __builtin_amdgcn_s_waitcnt(0); // the previous round's LDS reads have completed
             __builtin_amdgcn_wave_barrier();
@@ -973,18 +1067,60 @@ PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, co
         }
         if (w.act)
             words(r + w.i * n);
-        if (dbl && r + m < nout) {
-            // the other half's readers (the previous round) have completed: fetch the next round
-            // into it, then wait for everything but those DMA instructions
-            __builtin_amdgcn_wave_barrier();
-            issue(r + m, hb ^ hoff);
-            wait_vm(ninst);
+        if (dbl) {
+            // the buffer of round k-1 (its readers and writers have completed) takes round
+            // k+NB-1; then wait for everything but the rounds still in flight behind round k
+            const uint32_t ahead = R - 1 - k < NB - 1 ? R - 1 - k : NB - 1;
+            if (k + NB - 1 < R) {
+                __builtin_amdgcn_s_waitcnt(0xC07F); // lgkmcnt(0)
+                __builtin_amdgcn_wave_barrier();
+                issue((k + NB - 1) * m, ((kb + NB - 1) % NB) * hoff);
+            }
+            // younger than round k's fetch: the fetches of the rounds ahead, and the stores of the
+            // rounds computed since it was issued (n outputs x 3 / 1 wave-level stores each)
+            const uint32_t st = n * (FU ? 3u : 1u);
+            wait_vm(ninst * ahead + st * (k < NB - 1 ? k : NB - 1));
         } else {
             __builtin_amdgcn_s_waitcnt(0);
         }
+        hb = kb * hoff;
+        kb = kb + 1 == NB ? 0u : kb + 1;
         __builtin_amdgcn_wave_barrier();
+        if constexpr (L0 > 0) {
+            // the shared levels of this round's (G x KS x m) staged groups of J chunks, in place
+            // (every lane, active or not; one wave's LDS accesses complete in issue order)
+            float4* curw = reinterpret_cast<float4*>(stg) + (hb >> 2);
+            const uint32_t ng = (64u / LP) * KS * m;
+            for (uint32_t gi = c.lane; gi < ng; gi += 64u) {
+                const uint32_t g = gi % (64u / LP), q = gi / (64u / LP);
+                float4 v[J];
+#pragma unroll
+                for (uint32_t j = 0; j < J; ++j)
+                    v[j] = curw[stg_idx<LP>(q * J + j, g, per)];
+#pragma unroll
+                for (uint32_t l = 1; l <= L0; ++l)
+#pragma unroll
+                    for (uint32_t i = 0; i < (J >> l); ++i)
+                        v[i] = f4_f(v[2 * i], v[2 * i + 1]);
+#pragma unroll
+                for (uint32_t j = 0; j < J0; ++j)
+                    curw[stg_idx<LP>(q * J + j, g, per)] = v[j];
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
         if (!w.act)
             continue;
+#if defined(PCG_DEV_ABL_DEEP) && PCG_DEV_ABL_DEEP == 2 // dev ablation (wrong results): no arithmetic
+        for (uint32_t uu = 0; uu < n; ++uu) {
+            const uint32_t c2 = r + w.i * n + uu;
+            d1.st(c2, make_float4(0.f, 0.f, 0.f, 0.f));
+            if constexpr (FU) {
+                d1.st(c2 + hq2, make_float4(0.f, 0.f, 0.f, 0.f));
+                d2.st(c2, make_float4(0.f, 0.f, 0.f, 0.f));
+            }
+        }
+        continue;
+#endif
         const float4* cur = stg4 + (hb >> 2);
         for (uint32_t uu = 0; uu < n; ++uu) {
             const uint32_t u = w.i * n + uu, c2 = r + u;
@@ -994,12 +1130,12 @@ PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, co
             float4 x[KS];
 #pragma unroll
             for (uint32_t k = 0; k < KS; ++k) {
-                float4 v[J];
+                float4 v[J0];
 #pragma unroll
-                for (uint32_t j = 0; j < J; ++j)
+                for (uint32_t j = 0; j < J0; ++j)
                     v[j] = cur[stg_idx<LP>((u * KS + k) * J + j, mg, per)];
 #pragma unroll
-                for (int l = 1; l <= V; ++l)
+                for (uint32_t l = L0 + 1; l <= (uint32_t)V; ++l)
 #pragma unroll
                     for (uint32_t i = 0; i < (J >> l); ++i)
                         v[i] = ((RM >> (l - 1)) & 1) ? f4_g(v[2 * i], v[2 * i + 1], bw[k][J - (J >> (l - 1)) + i], gs)
@@ -1007,6 +1143,10 @@ PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, co
                 x[k] = v[0];
             }
             const float4 y0 = OPC == OP_F ? f4_f(x[0], x[1]) : f4_g(x[0], x[1], lw[0], gs);
+#if defined(PCG_DEV_ABL_DEEP) && PCG_DEV_ABL_DEEP == 3 // dev ablation (wrong results): no stores
+            if (c.N != 0)
+                continue;
+#endif
             d1.st(c2, y0);
             if constexpr (FU) {
                 const float4 y1 = OPC == OP_F ? f4_f(x[2], x[3]) : f4_g(x[2], x[3], lw[1], gs);
@@ -1015,7 +1155,14 @@ PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, co
             }
         }
     }
+#if PCG_STG_TAIL_DRAIN
     __builtin_amdgcn_s_waitcnt(0);
+#else
+    // every fetch has landed (the last round waited for its own); the LDS reads have completed
+    // before later ops reuse the region -- the op's global stores drain behind the next ops
+    // (same-wave accesses to one address stay ordered), not here
+    __builtin_amdgcn_s_waitcnt(0xC07F); // lgkmcnt(0)
+#endif
 }
 
 // the bits level l of a recomputed stage-(top-V) node at o reads: the left child of its
@@ -1897,10 +2044,18 @@ PCG_DEV void bit_level32(uint32_t (&k)[8], uint32_t p)
         bit_level32<LP, K, 2 * B>(k, p);
     }
 }
-template <int LP>
+// Code bits of a candidate: its path (log2 LP bits) and its index in a K-candidate list
+// (log2 K: 1 for Repetition, 2 for Rate-1, 3 for SPC) -- the fewer, the more value bits the
+// key keeps and the rarer the near ties (LP = 32, K = 2: 26 value bits, not 24)
+template <int K>
+constexpr uint32_t k32_lk()
+{
+    return K <= 2 ? 1u : K <= 4 ? 2u : 3u;
+}
+template <int LP, int K = 8>
 constexpr uint32_t k32_cb()
 {
-    return LP <= 2 ? 4u : LP <= 4 ? 5u : LP <= 8 ? 6u : LP <= 16 ? 7u : 8u;
+    return (LP <= 2 ? 1u : LP <= 4 ? 2u : LP <= 8 ? 3u : LP <= 16 ? 4u : 5u) + k32_lk<K>();
 }
 // Top-8 of an 8-lane group's 64 keys (LP = 8, K = 8: SPC leaves, np <= 8): instead of sorting
 // all 64, three butterfly levels each merge the lane's sorted 8 with its partner's into the top
@@ -1987,12 +2142,12 @@ PCG_DEV bool k32_select(const Ls<LP>& c, const float (&cv)[8], uint32_t P, uint3
 {
     if constexpr (PCG_SEL_TOP8 && LP == 8 && K == 8)
         return k32_top8<LP>(c, cv, P, np, R, val, src, jsel);
-    constexpr uint32_t CB = k32_cb<LP>(), cm = (1u << CB) - 1u;
+    constexpr uint32_t CB = k32_cb<LP, K>(), cm = (1u << CB) - 1u, LK = k32_lk<K>();
     const bool act = c.p < P;
     uint32_t q[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j)
-        q[j] = (act && j < K) ? ((ordz(cv[j]) & ~cm) | (~((c.p << 3) | (uint32_t)j) & cm)) : 0u;
+        q[j] = (act && j < K) ? ((ordz(cv[j]) & ~cm) | (~((c.p << LK) | (uint32_t)j) & cm)) : 0u;
     local_order32<K>(q);
     bit_level32<LP, K, 1>(q, c.p);
     bool near = false;
@@ -2014,8 +2169,8 @@ PCG_DEV bool k32_select(const Ls<LP>& c, const float (&cv)[8], uint32_t P, uint3
             mk = x;
     }
     const uint32_t code = ~mk & cm;
-    src = code >> 3;
-    jsel = code & 7u;
+    src = code >> LK;
+    jsel = code & ((1u << LK) - 1u);
     // the exact value of the candidate, from its path's lane
     float vv = 0.0f;
 #pragma unroll
@@ -3044,6 +3199,12 @@ std::string sclls_rtc_defines(bool* nondefault)
     d("PCG_DEEP_SHARE", PCG_DEEP_SHARE, 1);
     d("PCG_F_OLD", PCG_F_OLD, 0);
     d("PCG_SEL_TOP8", PCG_SEL_TOP8, 1);
+    d("PCG_STG_SHARED_F", PCG_STG_SHARED_F, 1);
+    d("PCG_STG_RING", PCG_STG_RING, 2);
+    d("PCG_STG_TAIL_DRAIN", PCG_STG_TAIL_DRAIN, 0);
+#ifdef PCG_DEV_ABL_DEEP
+    d("PCG_DEV_ABL_DEEP", PCG_DEV_ABL_DEEP, 0);
+#endif
     d("PCG_SEL_BITONIC_LP", PCG_SEL_BITONIC_LP, 16);
     d("PCG_SEL_BITONIC_K", PCG_SEL_BITONIC_K, 4);
     d("PCG_SEL_VMERGE", PCG_SEL_VMERGE, 0);

@@ -585,6 +585,13 @@ def main(argv=None):
                             os.environ["PCG_HOST_PIPE"] = old
                 line["host_buffers_cw_per_s"] = host_rate(os.environ.get("PCG_HOST_PIPE", "2"))
                 line["host_buffers_serial_cw_per_s"] = host_rate("0")
+                # a page-locked caller buffer (e.g. a simulator's reused frame buffer): copied from
+                # directly, no staging copy -- the PCIe-bound rate
+                pinned = torch.from_numpy(host_llr).pin_memory()
+                host_llr_pageable, host_llr = host_llr, pinned.numpy()
+                line["host_buffers_pinned_cw_per_s"] = host_rate(os.environ.get("PCG_HOST_PIPE", "2"))
+                host_llr = host_llr_pageable
+                del pinned
             if not args.no_cpu_baseline and world == 1:
                 if host_llr is None:  # device-generated frames: copy a bounded sample back
                     cpu_llr = d_llr[:4096].cpu().numpy()
