@@ -1086,7 +1086,9 @@ int pcg_decode_i8(pcg_plan* p,
 //   1  the caller's pageable buffer copied by the runtime on the copy stream (the host thread
 //      blocks in the copy while the previous chunk decodes);
 //   2  plan-owned pinned staging filled by PCG_HOST_THREADS host threads (default 8; with
-//      non-temporal stores, PCG_HOST_NT=0: plain memcpy), then a DMA copy on the copy stream.
+//      non-temporal stores, PCG_HOST_NT=0: plain memcpy), then a DMA copy on the copy stream;
+//   3  each chunk's whole pages page-locked in place for its copy (hipHostRegister, overlapped
+//      with the previous chunk's copy), the partial end pages staged as in 2.
 // A caller buffer that is already pinned (hipHostMalloc / hipHostRegister) is copied from
 // directly in modes 1 and 2.  PCG_HOST_CHUNK overrides the chunk size in frames (default:
 // 64 MB of input, between 4096 and 65536 frames).
@@ -1244,7 +1246,8 @@ static int decode_host(pcg_plan* p, const void* llr, size_t elem, uint64_t F, ui
     if (mode == 0)
         return decode_host_serial(p, llr, elem, F, info, ok, metrics, chunk);
     const bool direct = host_pinned(llr);
-    const bool stage = mode == 2 && !direct;
+    const bool stage = (mode == 2 || mode == 3) && !direct;
+    const bool reg = mode == 3 && !direct;
     const int threads = env_int("PCG_HOST_THREADS", 8);
     const bool nt = env_int("PCG_HOST_NT", 1) != 0;
     int rc = pipe_alloc(p, chunk, fb, stage);
@@ -1252,6 +1255,32 @@ static int decode_host(pcg_plan* p, const void* llr, size_t elem, uint64_t F, ui
         return rc;
     HostPipe* q = p->pipe;
     hipError_t e;
+    // mode 3: each chunk's whole pages are page-locked in place (hipHostRegister, while the
+    // previous chunk's copy runs) and copied from directly; the partial pages at its ends go
+    // through the staging buffer.  Every registration ends once its copy has completed (and on
+    // any error return, after the copy stream has drained).
+    struct Reg {
+        void* p = nullptr;
+    } regs[2];
+    struct RegGuard {
+        HostPipe* q;
+        Reg* r;
+        ~RegGuard()
+        {
+            if (!r[0].p && !r[1].p)
+                return;
+            (void)hipStreamSynchronize(q->copy);
+            for (int k = 0; k < 2; ++k)
+                if (r[k].p)
+                    (void)hipHostUnregister(r[k].p);
+        }
+    } guard{q, regs};
+    auto unreg = [&](int b) {
+        if (regs[b].p) {
+            (void)hipHostUnregister(regs[b].p);
+            regs[b].p = nullptr;
+        }
+    };
     // the slots' buffers are reused after the plan's previous decodes, whatever stream ran them
     if ((rc = order_on(p, q->copy)) != 0)
         return rc;
@@ -1267,6 +1296,7 @@ static int decode_host(pcg_plan* p, const void* llr, size_t elem, uint64_t F, ui
         hipError_t x = hipEventSynchronize(q->ev_done[b]);
         if (x != hipSuccess)
             return hip_fail(x, "hipEventSynchronize(host pipeline)");
+        unreg(b); // (its copy has completed)
         const uint64_t f0 = pend[b].f0, n = pend[b].n;
         memcpy(info + f0 * kb, q->h_out[b], n * kb);
         if (ok)
@@ -1283,12 +1313,37 @@ static int decode_host(pcg_plan* p, const void* llr, size_t elem, uint64_t F, ui
         if ((rc = retire(b)) != 0)
             return rc;
         const char* src = (const char*)llr + f0 * fb;
-        if (stage) {
-            par_memcpy(q->h_in[b], src, n * fb, threads, nt);
-            src = (const char*)q->h_in[b];
+        const size_t nb = n * fb;
+        bool done = false;
+        if (reg) {
+            const uintptr_t a = (uintptr_t)src, z = a + nb, pg = 4096;
+            const uintptr_t pa = (a + pg - 1) & ~(pg - 1), pz = z & ~(pg - 1);
+            if (pz > pa && hipHostRegister((void*)pa, pz - pa, hipHostRegisterDefault) == hipSuccess) {
+                regs[b].p = (void*)pa;
+                char* d = (char*)q->d_in[b];
+                char* hs = (char*)q->h_in[b];
+                memcpy(hs, src, pa - a);
+                memcpy(hs + (pz - a), (const char*)pz, z - pz);
+                if ((pa > a && (e = hipMemcpyAsync(d, hs, pa - a, hipMemcpyHostToDevice, q->copy)) != hipSuccess) ||
+                    (e = hipMemcpyAsync(d + (pa - a), (const void*)pa, pz - pa, hipMemcpyHostToDevice, q->copy)) !=
+                        hipSuccess ||
+                    (z > pz &&
+                     (e = hipMemcpyAsync(d + (pz - a), hs + (pz - a), z - pz, hipMemcpyHostToDevice, q->copy)) !=
+                         hipSuccess))
+                    return hip_fail(e, "hipMemcpyAsync(H2D)");
+                done = true;
+            } else {
+                (void)hipGetLastError(); // (not registrable: staged like mode 2)
+            }
         }
-        if ((e = hipMemcpyAsync(q->d_in[b], src, n * fb, hipMemcpyHostToDevice, q->copy)) != hipSuccess)
-            return hip_fail(e, "hipMemcpyAsync(H2D)");
+        if (!done) {
+            if (stage) {
+                par_memcpy(q->h_in[b], src, nb, threads, nt);
+                src = (const char*)q->h_in[b];
+            }
+            if ((e = hipMemcpyAsync(q->d_in[b], src, nb, hipMemcpyHostToDevice, q->copy)) != hipSuccess)
+                return hip_fail(e, "hipMemcpyAsync(H2D)");
+        }
         if ((e = hipEventRecord(q->ev_h2d[b], q->copy)) != hipSuccess ||
             (e = hipStreamWaitEvent(q->dec, q->ev_h2d[b], 0)) != hipSuccess)
             return hip_fail(e, "host pipeline event");

@@ -81,6 +81,11 @@ def parse(argv=None):
     ap.add_argument("--no-traffic", dest="traffic", action="store_false")
     ap.add_argument("--no-host-rate", action="store_true", help="skip the PCIe-inclusive host-buffer rate")
     ap.add_argument("--no-copy-bw", action="store_true", help="skip the device copy-bandwidth probe")
+    ap.add_argument("--in-flight", action="store_true",
+                    help="also time the same steps with a second batch in flight (second plan and stream): "
+                         "reported as roofline.throughput_2_in_flight_cw_per_s, never as value (off by default: "
+                         "its overlapping launches would skew a profiler's per-launch average)")
+    ap.add_argument("--no-in-flight", dest="in_flight", action="store_false")
     ap.add_argument("--streams", type=int, default=0,
                     help="batches in flight: S plans on S HIP streams, step i on stream i %% S (default: 2 for "
                          "the adaptive modes, whose latency-bound list stage then overlaps the next batch's "
@@ -188,7 +193,8 @@ def measure_traffic(args, kernel, frames):
             od = os.path.join(td, ctr)
             cmd = [rocprof, "--pmc", ctr, "-d", od, "-o", "run", "--output-format", "csv", "--",
                    sys.executable, os.path.abspath(__file__), "--mode", args.mode, "--steps", "2", "--warmup", "1",
-                   "--ebn0", str(args.ebn0), "--no-cpu-baseline", "--no-traffic", "--no-host-rate", "--no-copy-bw"]
+                   "--ebn0", str(args.ebn0), "--no-cpu-baseline", "--no-traffic", "--no-host-rate", "--no-copy-bw",
+                   "--no-in-flight"]
             env = dict(os.environ, TMPDIR="/tmp")
             for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
                 env.pop(k, None)
@@ -384,6 +390,7 @@ def main(argv=None):
     frozen = frozen_bits(1024, K, 0.0, "5G") if args.mode == "nr5g" else frozen_bits(N, K, 0.0, "BB")
 
     S = 1  # batches in flight (--streams)
+    in_flight2 = None
     if args.dry_run:
         # plumbing only: a host-only plan (classification, no GPU), a sleep as the step
         plan = Plan(N, L, frozen, systematic=True, crc=crc, device=-1, adaptive=adaptive, fixed=fixed)
@@ -479,6 +486,27 @@ def main(argv=None):
         # correctness spot check of the last step (decoded == transmitted fraction)
         fer = float((d_info != d_ref).any(dim=1).float().mean().item())
         ok_rate = float(d_ok.float().mean().item())
+        # (one stream) the same steps with a second batch in flight on a second stream and plan:
+        # reported beside `value`, never as it -- a launch ends with a tail of waves finishing
+        # their last codeword group, which the next batch's waves fill
+        in_flight2 = None
+        if S == 1 and world == 1 and args.steps and args.in_flight:
+            q2 = Plan(N, L, frozen, systematic=True, crc=crc, device=local, adaptive=adaptive, fixed=fixed)
+            specialize(q2)
+            plans.append(q2)
+            outs.append((torch.empty_like(d_info), torch.empty_like(d_ok),
+                         torch.empty_like(d_met) if d_met is not None else None))
+            streams.append(torch.cuda.Stream(device=dev))
+            S = 2
+            for i in range(2):
+                step(i)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(args.steps):
+                step(i)
+            torch.cuda.synchronize()
+            in_flight2 = F * args.steps / (time.perf_counter() - t0)
+            S = 1
 
     from antpolarcodes_amd.distributed import reduce_stats
     st = reduce_stats({"wall": (wall, "max"), "frames": (F * args.steps, "sum")})
@@ -498,6 +526,8 @@ def main(argv=None):
         if adaptive:  # the events bracket the whole adaptive decode, not the list kernel alone
             roof["kernel_ms_scope"] = ("the whole adaptive decode: the Fast-SSC stage, the compaction of its CRC "
                                        f"failures and {kernel} (rocprof gives each kernel's own average)")
+        if in_flight2 is not None:
+            roof["throughput_2_in_flight_cw_per_s"] = in_flight2
         if S > 1:
             roof["kernel_ms_scope"] = (f"{S} batches in flight on {S} streams: wall time per batch; one decode's "
                                        f"latency (events on its stream) is decode_latency_ms")

@@ -20,7 +20,7 @@ def code(oracle):
     return N, fr, llr
 
 
-@pytest.mark.parametrize("mode", ["0", "1", "2"])
+@pytest.mark.parametrize("mode", ["0", "1", "2", "3"])
 def test_host_pipeline_three_chunks_scl(oracle, monkeypatch, code, mode):
     """SCL-8 over 3000 frames in chunks of 1024 (three chunks, the last one partial): info, ok
     and metrics bit-exact against the oracle, in every staging mode; then a second call on the
@@ -42,7 +42,7 @@ def test_host_pipeline_three_chunks_scl(oracle, monkeypatch, code, mode):
     assert np.array_equal(gi, oi) and np.array_equal(gok, ook), mode
 
 
-@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("mode", ["1", "2", "3"])
 def test_host_pipeline_sc_and_int8(oracle, monkeypatch, code, mode):
     """Fast-SSC float frames and the 8-bit list decoder on int8 frames through the pipeline
     (odd chunk size: 7 chunks of 448 frames, the last one partial), and a batch smaller than

@@ -14,7 +14,7 @@ for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ
            "TCC_HIT_sum TCC_MISS_sum" "TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SMEM SQ_INSTS_BRANCH"; do
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $grp -d $OUT/p$i -o run --output-format csv -- \
-      python bench.py --mode $MODE --steps 2 --warmup 1 --no-cpu-baseline --no-traffic --no-host-rate --no-copy-bw \
+      python bench.py --mode $MODE --steps 2 --warmup 1 --no-cpu-baseline --no-traffic --no-host-rate --no-copy-bw --no-in-flight \
       > $OUT/p$i.log 2>&1 || { echo "pass $i failed: $grp"; tail -5 $OUT/p$i.log; exit 1; }
 done
 python3 - "$OUT" <<'EOF'

@@ -9,5 +9,5 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 400 python bench.py --mode $MODE --steps $STEPS > $OUT/$MODE.json 2> $OUT/$MODE.err || exit 1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/${MODE}_stats -o run --output-format csv -- \
-    python bench.py --mode $MODE --steps 5 --warmup 1 --no-cpu-baseline --no-traffic --no-host-rate --no-copy-bw \
+    python bench.py --mode $MODE --steps 5 --warmup 1 --no-cpu-baseline --no-traffic --no-host-rate --no-copy-bw --no-in-flight \
     > $OUT/${MODE}_stats.log 2>&1 || exit 1

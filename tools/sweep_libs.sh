@@ -14,7 +14,7 @@ for cfg in "$@"; do
   dl=""
   [ "$lib" != "-" ] && dl="PCG_DEV_LIB=lib_dev/libpcg_$lib.so"
   echo "== $cfg" >> $OUT/sweep_$MODE.txt
-  env $dl $envs timeout -k 10 300 python bench.py --mode $MODE --steps 10 --no-cpu-baseline --no-host-rate --no-copy-bw \
+  env $dl $envs timeout -k 10 300 python bench.py --mode $MODE --steps 10 --no-cpu-baseline --no-host-rate --no-copy-bw --no-in-flight \
       > $OUT/sweep_${MODE}_$i.json 2> $OUT/sweep_${MODE}_$i.err || exit 1
   python3 -c "
 import json,sys
