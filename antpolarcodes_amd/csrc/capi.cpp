@@ -453,18 +453,23 @@ const char* pcg_last_error(void) { return g_last_error.c_str(); }
 // Development aid, not part of include/pcg.h: with PCG_OPPROF=1 in the environment
 // the kernels accumulate s_memtime cycles and counts per op code; this copies the
 // 64 x {cycles, count} table out and clears it.
-int pcg_dev_opprof_fetch(unsigned long long* out128)
+// (pcg_dev_opprof_fetch_n: the first n <= 256 entries -- the list kernel's profiler keeps
+// requested global read / write bytes per op bucket in entries 64-127 / 128-191.)
+int pcg_dev_opprof_fetch_n(unsigned long long* out, int n)
 {
+    if (n < 0 || n > 256)
+        return fail(PCG_E_ARG, "opprof: n > 256");
     if (!g_prof) {
-        std::memset(out128, 0, 128 * sizeof(unsigned long long));
+        std::memset(out, 0, (size_t)n * sizeof(unsigned long long));
         return PCG_OK;
     }
     if (hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpy(out128, g_prof, 128 * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+        hipMemcpy(out, g_prof, (size_t)n * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
         return fail(PCG_E_HIP, "opprof copy failed");
-    (void)hipMemset(g_prof, 0, 128 * sizeof(unsigned long long));
+    (void)hipMemset(g_prof, 0, 256 * sizeof(unsigned long long));
     return PCG_OK;
 }
+int pcg_dev_opprof_fetch(unsigned long long* out128) { return pcg_dev_opprof_fetch_n(out128, 128); }
 
 // Development aid, not part of include/pcg.h: the cache file name of the plan's specialised
 // kernel (antpolarcodes_amd/rtc_warm.py keeps the shipped cache to the listed codes).
@@ -979,8 +984,8 @@ static int decode_impl(pcg_plan* p,
     a.llr8 = llr8;
     a.metric0 = p->metric0;
     if (p->dev_opprof) {
-        if (!g_prof && hipMalloc(&g_prof, 128 * sizeof(unsigned long long)) == hipSuccess)
-            (void)hipMemset(g_prof, 0, 128 * sizeof(unsigned long long));
+        if (!g_prof && hipMalloc(&g_prof, 256 * sizeof(unsigned long long)) == hipSuccess)
+            (void)hipMemset(g_prof, 0, 256 * sizeof(unsigned long long));
         a.prof = g_prof;
     }
     a.flags = p->dev_flags;

@@ -190,6 +190,25 @@ struct Ls {
     }
 };
 
+#ifdef PCG_LS_PROF
+// dev (op profiler): global bytes the running op requests (loads / LDS DMA in [0], stores in
+// [1]), counted per wave by its first active lane over the active lanes
+PCG_DEV uint32_t* ls_gb_ctr()
+{
+    __shared__ uint32_t n[2];
+    return n;
+}
+PCG_DEV void ls_gb(uint32_t per_lane, int wr)
+{
+    const uint64_t ex = __builtin_amdgcn_read_exec();
+    if (__builtin_amdgcn_mbcnt_hi((uint32_t)(ex >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ex, 0u)) == 0u)
+        atomicAdd(&ls_gb_ctr()[wr], per_lane * (uint32_t)__builtin_popcountll(ex));
+}
+#define LS_GB(n, wr) ls_gb((n), (wr))
+#else
+#define LS_GB(n, wr) (void)0
+#endif
+
 // The bits of D[s] of one path, read a word at a time by G ops and recomputed right
 // children (wave-uniform LDS / global choice per read).
 // (Codeword rows: the row of the path's lane, relative positions from the node's offset.)
@@ -199,7 +218,14 @@ struct DBits {
     uint32_t lane;
     bool glob;
     uint32_t base; // position of relative bit 0 (rows: the node's offset)
-    PCG_DEV uint32_t word(uint32_t w) const { return glob ? g[((uint64_t)w << 6) + lane] : l[(w << 6) + lane]; }
+    PCG_DEV uint32_t word(uint32_t w) const
+    {
+        if (glob) {
+            LS_GB(4, 0);
+            return g[((uint64_t)w << 6) + lane];
+        }
+        return l[(w << 6) + lane];
+    }
     // bits from relative position i (the 32 - (i & 31) bits of its word); the word holding it
     PCG_DEV uint32_t at(uint32_t i) const { return word((base + i) >> 5) >> ((base + i) & 31u); }
     PCG_DEV uint32_t wat(uint32_t i) const { return word((base + i) >> 5); }
@@ -244,8 +270,16 @@ struct LdsSt {
 struct GlSt {
     float* b;
     uint32_t lane;
-    PCG_DEV float4 ld(uint32_t c, uint32_t l) const { return *reinterpret_cast<const float4*>(b + ((uint64_t)((c << 6) + l)) * 4u); }
-    PCG_DEV void st(uint32_t c, const float4& v) const { *reinterpret_cast<float4*>(b + ((uint64_t)((c << 6) + lane)) * 4u) = v; }
+    PCG_DEV float4 ld(uint32_t c, uint32_t l) const
+    {
+        LS_GB(16, 0);
+        return *reinterpret_cast<const float4*>(b + ((uint64_t)((c << 6) + l)) * 4u);
+    }
+    PCG_DEV void st(uint32_t c, const float4& v) const
+    {
+        LS_GB(16, 1);
+        *reinterpret_cast<float4*>(b + ((uint64_t)((c << 6) + lane)) * 4u) = v;
+    }
 };
 // Stages >= mt are never stored.  With virt = 1 the root's children (stage top-1)
 // are recomputed wherever they are read: the left child F(y_j, y_j+N/2) is path
@@ -267,7 +301,11 @@ PCG_DEV float4 f4_g(const float4& a, const float4& b, uint32_t wb, uint32_t k0 =
 // Channel loads.  (Measured round 2: non-temporal loads here -- frames kept out of L2 to
 // leave it to the stage slab -- raise traffic to 330 KB/cw and cost 10 %: the channel
 // re-reads do hit L2, the slab does not; profiles/r02_scl8_nt_channel.json.)
-PCG_DEV float4 chan_ld(const float* y, uint32_t c) { return reinterpret_cast<const float4*>(y)[c]; }
+PCG_DEV float4 chan_ld(const float* y, uint32_t c)
+{
+    LS_GB(16, 0);
+    return reinterpret_cast<const float4*>(y)[c];
+}
 
 struct ChSt { // the channel LLRs of the lane's own codeword (stage top)
     const float* y;
@@ -773,6 +811,7 @@ PCG_DEV void ls_fgf_root(const Ls<LP>& c, GlSt d1, Dst2 d2, const DBits& lb, con
                 a += hq1;
             const uint32_t lo = shfl((uint32_t)yp, (int)(g * LP)), hi = shfl((uint32_t)(yp >> 32), (int)(g * LP));
             const float* src = reinterpret_cast<const float*>((uintptr_t)(((uint64_t)hi << 32) | lo)) + 4u * a;
+            LS_GB(16, 0);
             __builtin_amdgcn_global_load_lds(src, stg + t * 256u, 16, 0, 0);
         }
         if (grp && w.act)
@@ -867,6 +906,7 @@ PCG_DEV uint32_t ls_root_round(const Ls<LP>& c, uint32_t s, uint32_t h, bool fus
 // (cdna_hip_programming.md, LDS-DMA recipe).
 PCG_DEV void glds16(const float* src, float* lds)
 {
+    LS_GB(16, 0);
     const uint32_t dst = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float*)lds);
     uint32_t keep;
@@ -1046,8 +1086,10 @@ PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, co
             const float* src = reinterpret_cast<const float*>((uintptr_t)(((uint64_t)hi << 32) | lo)) + 4u * a;
             if (PCG_STG_DB && !Ls<LP>::DB) // (every round explicitly waited for: s_waitcnt / wait_vm below)
                 glds16(src, stg + hb + t * 256u);
-            else
+            else {
+                LS_GB(16, 0);
                 __builtin_amdgcn_global_load_lds(src, stg + hb + t * 256u, 16, 0, 0);
+            }
         }
     };
     // round k lives in buffer k % NB; the first NB-1 rounds are fetched up front
@@ -1283,8 +1325,16 @@ struct DColL {
 };
 struct DColG {
     gl_u32* b;
-    PCG_DEV uint32_t ld(uint32_t w, uint32_t l) const { return b[((uint64_t)w << 6) + l]; }
-    PCG_DEV void st(uint32_t w, uint32_t l, uint32_t v) const { b[((uint64_t)w << 6) + l] = v; }
+    PCG_DEV uint32_t ld(uint32_t w, uint32_t l) const
+    {
+        LS_GB(4, 0);
+        return b[((uint64_t)w << 6) + l];
+    }
+    PCG_DEV void st(uint32_t w, uint32_t l, uint32_t v) const
+    {
+        LS_GB(4, 1);
+        b[((uint64_t)w << 6) + l] = v;
+    }
 };
 template <int LP, typename Fn>
 PCG_DEV void with_d(const Ls<LP>& c, uint32_t s, Fn&& fn)
@@ -2857,7 +2907,7 @@ PCG_DEV void sclls_body(const KernelArgs& a)
     uint64_t* lprof = reinterpret_cast<uint64_t*>(smem + a.wave_lds_floats);
     c.lprof = lprof;
     if (threadIdx.x == 0)
-        for (int b = 0; b < 64; ++b)
+        for (int b = 0; b < 192; ++b) // cycles, then requested read / write bytes per bucket
             lprof[b] = 0;
     wsync();
 #endif
@@ -2911,6 +2961,10 @@ PCG_DEV void sclls_body(const KernelArgs& a)
             const uint32_t code = op_code(w), s = op_stage(w), o = op_off(w);
 #ifdef PCG_LS_PROF
             const uint64_t t0 = __builtin_amdgcn_s_memtime();
+            if (c.lane == 0) {
+                ls_gb_ctr()[0] = 0;
+                ls_gb_ctr()[1] = 0;
+            }
 #endif
             // an F/G whose output stage is in the global slab and whose next op is the
             // child's F runs fused with it (ls_fgf)
@@ -2930,8 +2984,11 @@ PCG_DEV void sclls_body(const KernelArgs& a)
                 uint32_t b = code;
                 if (code == OP_F || code == OP_G)
                     b += s >= c.mt ? 16u : s >= c.Sl ? 8u : (s - 1 >= c.Sl ? 24u : 0u);
-                if (c.lane == 0)
+                if (c.lane == 0) {
                     lprof[b] += t1 - t0;
+                    lprof[64 + b] += ls_gb_ctr()[0];
+                    lprof[128 + b] += ls_gb_ctr()[1];
+                }
             }
 #endif
         }
@@ -3013,7 +3070,7 @@ PCG_DEV void sclls_body(const KernelArgs& a)
 #ifdef PCG_LS_PROF
     wsync();
     if (c.lane == 0 && a.prof)
-        for (int b = 0; b < 64; ++b)
+        for (int b = 0; b < 192; ++b)
             if (lprof[b])
                 atomicAdd(&a.prof[b], (unsigned long long)lprof[b]);
 #endif
@@ -3267,7 +3324,7 @@ int launch_sclls(const KernelArgs& a, hipStream_t stream)
         return a.F ? -4 : 0;
     size_t lds = (size_t)a.wave_lds_floats * sizeof(float);
 #ifdef PCG_LS_PROF
-    lds += 64 * sizeof(uint64_t);
+    lds += 192 * sizeof(uint64_t);
 #endif
     const uint32_t lp = a.scl_lp > lp_of(a.L) ? a.scl_lp : lp_of(a.L);
 #if PCG_LS_INST

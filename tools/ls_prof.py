@@ -7,7 +7,10 @@ output; 60 = extractBestPath + output.  Sub-buckets, also counted inside their o
 bucket: 50 = path selection (ls_select, sort + merge rounds / bitonic merge), 51 = path
 duplication (ls_dup: slot row + codeword prefix copy), 52 = survivor register shuffle
 inside size-8 subtrees (st8_branch), 53 = weak-LLR search of Rate-1 / SPC leaves n >= 8
-(weak_fast, ls_weak on ties)."""
+(weak_fast, ls_weak on ties).  Beside the cycles: the global bytes each op bucket requests
+(loads, LDS DMA and stores through the slab / channel / D-region accessors, per codeword) --
+what the L1 asks of L2, against which the measured HBM traffic (FETCH_SIZE + WRITE_SIZE) of
+the bench line is the L2 / MALL-filtered part."""
 import ctypes as C
 import os
 import sys
@@ -27,13 +30,13 @@ p = Plan(N, L, fz, crc=8)
 d = torch.from_numpy(llr).cuda()
 di = torch.zeros((F, p.kb), dtype=torch.uint8, device="cuda")
 do = torch.zeros(F, dtype=torch.uint8, device="cuda")
-buf = (C.c_ulonglong * 128)()
+buf = (C.c_ulonglong * 256)()
 p.decode_device(d, di, do)
 torch.cuda.synchronize()
-_native.lib().pcg_dev_opprof_fetch(buf)  # discard the first launch
+_native.lib().pcg_dev_opprof_fetch_n(buf, 256)  # discard the first launch
 p.decode_device(d, di, do)
 torch.cuda.synchronize()
-_native.lib().pcg_dev_opprof_fetch(buf)
+_native.lib().pcg_dev_opprof_fetch_n(buf, 256)
 base = {1: "F", 2: "G", 4: "COMB", 40: "R0", 41: "R1", 42: "REP", 43: "SPC", 44: "ST8", 60: "output",
         50: "  [path selection]", 51: "  [path duplication]", 52: "  [st8 survivor shuffle]",
         53: "  [weak-LLR search]"}
@@ -51,3 +54,21 @@ for b in range(60):
 rows.append((buf[60], "output"))
 for cyc, nm in sorted(rows, reverse=True):
     print(f"  {nm:20s} {100 * cyc / max(whole, 1):5.1f}%")
+# requested global bytes per codeword and op bucket (G = 64 / LP codewords per group)
+lp = 1
+while lp < L:
+    lp <<= 1
+ncw = max(buf[62], 1) * (64 // lp)
+print(f"requested global bytes per codeword by op bucket (loads incl. LDS DMA / stores), {ncw} codewords:")
+tr = tw = 0
+brow = []
+for b in range(60):
+    r, w = buf[64 + b], buf[128 + b]
+    if r or w:
+        nm = base[b & 7] + cls[b & 24] if b < 32 and (b & 7) in (1, 2) else base.get(b, str(b))
+        brow.append((r + w, nm, r, w))
+        tr += r
+        tw += w
+for _, nm, r, w in sorted(brow, reverse=True):
+    print(f"  {nm:24s} read {r / ncw:9.0f} B  write {w / ncw:9.0f} B  ({100 * (r + w) / max(tr + tw, 1):5.1f}%)")
+print(f"  {'total':24s} read {tr / ncw:9.0f} B  write {tw / ncw:9.0f} B")
