@@ -84,10 +84,16 @@ PCG_DEV uint32_t sign4(uint32_t d)
 // 16 x int8 per lane and unit
 PCG_DEV uint4 f16(const uint4& a, const uint4& b)
 {
+#if defined(PCG_I8_ABL) && (PCG_I8_ABL & 1) // dev ablation (wrong results): F's byte arithmetic removed
+    return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
+#endif
     return make_uint4(f4(a.x, b.x), f4(a.y, b.y), f4(a.z, b.z), f4(a.w, b.w));
 }
 PCG_DEV uint4 g16(const uint4& a, const uint4& b, uint32_t bits16)
 {
+#if defined(PCG_I8_ABL) && (PCG_I8_ABL & 2) // dev ablation (wrong results): G's byte arithmetic removed
+    return make_uint4(a.x ^ b.x ^ bits16, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
+#endif
     return make_uint4(g4b(a.x, b.x, bits16, 0), g4b(a.y, b.y, bits16, 4), g4b(a.z, b.z, bits16, 8),
                       g4b(a.w, b.w, bits16, 12));
 }
