@@ -893,6 +893,9 @@ PCG_DEV uint32_t ls_root_round(const Ls<LP>& c, uint32_t s, uint32_t h, bool fus
 #ifndef PCG_STG_TAIL_DRAIN
 #define PCG_STG_TAIL_DRAIN 0 // 1: the recomputed-node ops end waiting for their stores too
 #endif
+#ifndef PCG_LS_STAGGER
+#define PCG_LS_STAGGER 2 // start-stagger step (x s_sleep 127) per pseudo-random unit, 0: off (sclls_body)
+#endif
 #ifndef PCG_STG_RING
 #define PCG_STG_RING 2 // at most this many buffers (measured: 3 buffers -1 % against 2 on config 3, r05g)
 #endif
@@ -2931,6 +2934,18 @@ PCG_DEV void sclls_body(const KernelArgs& a)
     const uint32_t W = a.N >= 32 ? a.N / 32 : 1u;
 
     const uint64_t Fn = a.fcount ? (uint64_t)*a.fcount : a.F;
+#if PCG_LS_STAGGER > 0
+    // Start stagger: every wave would otherwise run the first codeword group's ops in step with
+    // all the others (the same staged channel rounds, the same slab stages at the same time), and
+    // the first round of a launch then takes ~1.6x a steady-state round.  A pseudo-random delay
+    // of 0..15 steps of ~3.4 us desynchronises them (launches of >= 2 groups per wave only: a
+    // one-round launch, e.g. an adaptive plan's list stage, would just wait).
+    if (Fn >= 2ull * G * gridDim.x) {
+        const uint32_t steps = ((blockIdx.x * 2654435761u) >> 28) * (uint32_t)PCG_LS_STAGGER;
+        for (uint32_t i = 0; i < steps; ++i)
+            __builtin_amdgcn_s_sleep(127);
+    }
+#endif
     // codeword groups: from the plan's work queue (dynamic balance across SIMDs whose
     // resident wave counts differ), else a static grid stride
     const uint64_t stride = (uint64_t)gridDim.x * G;
@@ -3259,6 +3274,7 @@ std::string sclls_rtc_defines(bool* nondefault)
     d("PCG_STG_SHARED_F", PCG_STG_SHARED_F, 1);
     d("PCG_STG_RING", PCG_STG_RING, 2);
     d("PCG_STG_TAIL_DRAIN", PCG_STG_TAIL_DRAIN, 0);
+    d("PCG_LS_STAGGER", PCG_LS_STAGGER, 2);
 #ifdef PCG_DEV_ABL_DEEP
     d("PCG_DEV_ABL_DEEP", PCG_DEV_ABL_DEEP, 0);
 #endif
