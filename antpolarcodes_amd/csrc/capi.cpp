@@ -10,6 +10,7 @@
 #include <emmintrin.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -484,6 +485,33 @@ int pcg_dev_rtc_cache_name(const pcg_plan* p, char* out, size_t n)
     if (name.empty())
         return fail(PCG_E_UNSUPPORTED, "no plan-specialised kernel for this plan");
     snprintf(out, n, "%s", name.c_str());
+    return PCG_OK;
+}
+
+// Development aid, not part of include/pcg.h: the name a lookup in directory `dir` reads for the
+// plan's specialised kernel (the shipped cache is read under the version its HIPRTC_VERSION file
+// records; rtc_warm.py checks that this is the name it wrote).
+int pcg_dev_rtc_lookup_name(const pcg_plan* p, const char* dir, char* out, size_t n)
+{
+    if (!p || !dir || !out || n == 0)
+        return fail(PCG_E_ARG, "null argument");
+    std::string name;
+    for (const pcg_plan* q : {(const pcg_plan*)p->fast, p})
+        if (q && rtc_capable(q))
+            name += (name.empty() ? "" : " ") + pcg::rtc_lookup_name(rtc_source(q), dir);
+    if (name.empty())
+        return fail(PCG_E_UNSUPPORTED, "no plan-specialised kernel for this plan");
+    snprintf(out, n, "%s", name.c_str());
+    return PCG_OK;
+}
+
+// Development aid, not part of include/pcg.h: the hiprtc version this process compiles with (the
+// shipped cache's HIPRTC_VERSION, which rtc_warm.py rewrites when it differs).
+int pcg_dev_rtc_version(char* out, size_t n)
+{
+    if (!out || n == 0)
+        return fail(PCG_E_ARG, "null argument");
+    snprintf(out, n, "%s", pcg::rtc_version().c_str());
     return PCG_OK;
 }
 
@@ -1152,6 +1180,47 @@ static void par_memcpy(void* dst, const void* src, size_t bytes, int threads, bo
         x.join();
 }
 
+// Stage `bytes` of pageable input into the pinned buffer `h` and copy it to `d` on `st`, piece by
+// piece: the host threads (started once) each copy their share of piece k and count it done; the
+// calling thread issues piece k's DMA as soon as every share has landed, while the threads go on
+// with piece k+1.
+static hipError_t staged_copy(void* h, void* d, const char* src, size_t bytes, size_t piece, int threads, bool nt,
+                              hipStream_t st)
+{
+    if (piece >= bytes || threads <= 1) {
+        par_memcpy(h, src, bytes, threads, nt);
+        return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st);
+    }
+    auto cp = nt ? nt_memcpy : [](void* dd, const void* ss, size_t n) { memcpy(dd, ss, n); };
+    const size_t np = (bytes + piece - 1) / piece;
+    std::vector<std::atomic<int>> done(np);
+    for (auto& x : done)
+        x.store(0, std::memory_order_relaxed);
+    const int t = threads;
+    auto work = [&](int k) {
+        for (size_t i = 0; i < np; ++i) {
+            const size_t o = i * piece, pb = std::min(piece, bytes - o);
+            const size_t part = ((pb + t - 1) / t + 4095) & ~size_t(4095), a = part * (size_t)k;
+            if (a < pb)
+                cp((char*)h + o + a, src + o + a, std::min(part, pb - a));
+            done[i].fetch_add(1, std::memory_order_release);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int k = 0; k < t; ++k)
+        th.emplace_back(work, k);
+    hipError_t e = hipSuccess;
+    for (size_t i = 0; i < np && e == hipSuccess; ++i) {
+        while (done[i].load(std::memory_order_acquire) < t)
+            std::this_thread::yield();
+        const size_t o = i * piece;
+        e = hipMemcpyAsync((char*)d + o, (const char*)h + o, std::min(piece, bytes - o), hipMemcpyHostToDevice, st);
+    }
+    for (auto& x : th)
+        x.join();
+    return e;
+}
+
 static int pipe_alloc(pcg_plan* p, uint64_t frames, size_t in_fb, bool pinned_in)
 {
     HostPipe* q = p->pipe;
@@ -1255,6 +1324,9 @@ static int decode_host(pcg_plan* p, const void* llr, size_t elem, uint64_t F, ui
     const bool reg = mode == 3 && !direct;
     const int threads = env_int("PCG_HOST_THREADS", 8);
     const bool nt = env_int("PCG_HOST_NT", 1) != 0;
+    // staging piece (PCG_HOST_PIECE_MB, default 8 MB; 0: the whole chunk at once, round 5)
+    const int piece_mb = env_int("PCG_HOST_PIECE_MB", 8);
+    const size_t piece = piece_mb > 0 ? (size_t)piece_mb << 20 : ~size_t(0);
     int rc = pipe_alloc(p, chunk, fb, stage);
     if (rc != 0)
         return rc;
@@ -1341,11 +1413,13 @@ static int decode_host(pcg_plan* p, const void* llr, size_t elem, uint64_t F, ui
                 (void)hipGetLastError(); // (not registrable: staged like mode 2)
             }
         }
-        if (!done) {
-            if (stage) {
-                par_memcpy(q->h_in[b], src, nb, threads, nt);
-                src = (const char*)q->h_in[b];
-            }
+        if (!done && stage) {
+            // staged in pieces, each copied as soon as it is staged: the DMA of piece k overlaps
+            // the staging of piece k+1, so the copy engine starts after one piece (not one whole
+            // chunk) and the pipeline's fill is a piece long
+            if ((e = staged_copy(q->h_in[b], q->d_in[b], src, nb, piece, threads, nt, q->copy)) != hipSuccess)
+                return hip_fail(e, "hipMemcpyAsync(H2D)");
+        } else if (!done) {
             if ((e = hipMemcpyAsync(q->d_in[b], src, nb, hipMemcpyHostToDevice, q->copy)) != hipSuccess)
                 return hip_fail(e, "hipMemcpyAsync(H2D)");
         }

@@ -508,31 +508,19 @@ bool UndefinedDecoder::decode()
     return false;
 }
 
-void DecodedFloatContainer::getSoftBits(void* pData)
-{
-    if (!mSoft)
-        throw std::logic_error("no soft codeword: this GPU decoder keeps hard decisions only (soft output: "
-                               "Fast-SSC float decoders, N <= 16384)");
-    FloatContainer::getSoftBits(pData);
-}
+// Soft accessors of the GPU decoders' output container.  Fast-SSC float decoders (N <= 16384)
+// hold the reference's soft codeword word for word; every other GPU decoder holds the selected
+// path's signed hard decisions (+0.0 / -0.0, or the char bits 127 / -128).  Only the signs of the
+// reference's list / 8-bit "bit" buffers are observable (scl_avx_float.cpp:711-750 copies the
+// selected path's Bit(path, dataStage) into mBitContainer; decoder.cpp:147-151 returns it), so the
+// signs are the reference's.
+void DecodedFloatContainer::getSoftBits(void* pData) { FloatContainer::getSoftBits(pData); }
 
-void DecodedFloatContainer::getSoftInformation(void* pData)
-{
-    if (!mSoft)
-        throw std::logic_error("no soft codeword: this GPU decoder keeps hard decisions only (soft output: "
-                               "Fast-SSC float decoders, N <= 16384)");
-    FloatContainer::getSoftInformation(pData);
-}
+void DecodedFloatContainer::getSoftInformation(void* pData) { FloatContainer::getSoftInformation(pData); }
 
-void DecodedCharContainer::getSoftBits(void*)
-{
-    throw std::logic_error("no soft codeword: the GPU 8-bit decoders keep hard decisions only");
-}
+void DecodedCharContainer::getSoftBits(void* pData) { CharContainer::getSoftBits(pData); }
 
-void DecodedCharContainer::getSoftInformation(void*)
-{
-    throw std::logic_error("no soft codeword: the GPU 8-bit decoders keep hard decisions only");
-}
+void DecodedCharContainer::getSoftInformation(void* pData) { CharContainer::getSoftInformation(pData); }
 
 static void throw_pcg(int rc)
 {

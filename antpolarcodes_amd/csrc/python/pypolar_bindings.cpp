@@ -159,17 +159,28 @@ PYBIND11_MODULE(_pypolar, m)
                  std::memcpy(res.request().ptr, tmp.data(), s.dec->infoLength() / 8);
                  return res;
              })
-        .def("getSoftCodeword", // Decoder::getSoftCodeword after decode_vector (Fast-SSC float)
-             [](PyDecoder& s) {
+        .def("getSoftCodeword", // Decoder::getSoftCodeword after decode_vector: float32 (float
+                                // decoders) or int8 (8-bit decoders) per codeword bit
+             [](PyDecoder& s) -> py::object {
+                 if (dynamic_cast<CharContainer*>(s.dec->outputContainer())) {
+                     py::array_t<int8_t> out(s.dec->blockLength());
+                     s.dec->getSoftCodeword(out.mutable_data());
+                     return std::move(out);
+                 }
                  py::array_t<float> out(s.dec->blockLength());
                  s.dec->getSoftCodeword(out.mutable_data());
-                 return out;
+                 return std::move(out);
              })
         .def("getSoftInformation",
-             [](PyDecoder& s) {
+             [](PyDecoder& s) -> py::object {
+                 if (dynamic_cast<CharContainer*>(s.dec->outputContainer())) {
+                     py::array_t<int8_t> out(s.dec->infoLength());
+                     s.dec->getSoftInformation(out.mutable_data());
+                     return std::move(out);
+                 }
                  py::array_t<float> out(s.dec->infoLength());
                  s.dec->getSoftInformation(out.mutable_data());
-                 return out;
+                 return std::move(out);
              })
         .def("carriedMetric", // SCL: path 0's metric the next decode_vector starts from (Q8)
              [](PyDecoder& s) {

@@ -371,8 +371,11 @@ void finish(RtcJob& j)
 
 // Process exit waits for compiles still running (their thread is inside hiprtc, whose
 // teardown must not run under it).  It says so on stderr when it has to wait, and
-// PCG_RTC_EXIT_WAIT=<seconds> bounds the wait: past it the process ends at once (_exit,
-// status 0: the program itself has finished) without running the remaining exit handlers.
+// PCG_RTC_EXIT_WAIT=<seconds> bounds the wait: past it the process flushes every stdio stream and
+// ends at once (_exit) without running the remaining exit handlers.  An atexit handler cannot
+// read the status the program passed to exit(), so that status is REPLACED by
+// PCG_RTC_EXIT_STATUS (default 75, EX_TEMPFAIL): never 0, so leaving early never reports a
+// failed run as a success.
 void wait_running()
 {
     Registry& r = reg();
@@ -389,10 +392,15 @@ void wait_running()
         bound = atol(e);
     if (bound >= 0) {
         if (!r.idle.wait_for(lk, std::chrono::seconds(bound), [&] { return r.running == 0; })) {
-            fprintf(stderr, "[pcg] exit: %d compile(s) still running after %ld s; leaving without them\n",
-                    r.running, bound);
-            fflush(stderr);
-            _exit(0);
+            int status = 75; // EX_TEMPFAIL
+            if (const char* e = getenv("PCG_RTC_EXIT_STATUS"))
+                status = atoi(e);
+            fprintf(stderr,
+                    "[pcg] exit: %d compile(s) still running after %ld s; leaving without them, exit status %d "
+                    "(PCG_RTC_EXIT_STATUS) replaces the program's\n",
+                    r.running, bound, status);
+            fflush(nullptr); // every stdio stream: buffered stdout of C / C++ callers too
+            _exit(status);
         }
     } else {
         r.idle.wait(lk, [&] { return r.running == 0; });
@@ -497,6 +505,14 @@ std::string scl_rtc_source(const PlanHost& h, uint32_t lp, uint32_t Sl, uint32_t
 const char* rtc_arch() { return PCG_ARCH; }
 
 std::string rtc_cache_name(const std::string& src) { return cache_name(src); }
+
+std::string rtc_lookup_name(const std::string& src, const std::string& dir)
+{
+    const std::string v = dir_version(dir);
+    return cache_name(src, v.empty() ? api().version : v);
+}
+
+std::string rtc_version() { return api().version; }
 
 int rtc_compiles()
 {

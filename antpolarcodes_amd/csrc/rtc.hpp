@@ -44,8 +44,14 @@ int rtc_result(RtcJob& j, std::vector<char>* code, std::string* err);
 int rtc_compile(const std::string& src, std::vector<char>* code, std::string* err);
 // hiprtc compiles started by this process (tests: plans of one code share one compile)
 int rtc_compiles();
-// The cache file name of a generated source (shipped and user caches).
+// The cache file name of a generated source (the user cache, and what a compile writes).
 std::string rtc_cache_name(const std::string& src);
+// The name a lookup in directory `dir` reads for `src`: named by the hiprtc version the
+// directory records (its HIPRTC_VERSION file), else this process's (what disk_lookup reads in the
+// shipped cache).
+std::string rtc_lookup_name(const std::string& src, const std::string& dir);
+// The hiprtc version this process compiles with ("major.minor"; "none" without hiprtc).
+std::string rtc_version();
 // The GPU architecture the specialised kernels are compiled for (the library's ARCH).
 const char* rtc_arch();
 // Launch a loaded specialised kernel (grid = a.units, LDS = a.wave_lds_floats).

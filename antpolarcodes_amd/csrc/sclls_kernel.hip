@@ -1023,7 +1023,15 @@ PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, co
     // buffers (LP >= 16) the level bits are global loads that the compiler waits for with vmcnt(0),
     // which drains the in-flight rounds as well (measured with two buffers, config 5: 1.244e6 ->
     // 1.203e6 cw/s; config 3, rows: 2.844e7 -> 2.874e7; profiles/r05b_*)
+    // (The double-buffered wait counts this op's global stores: every computed round issues exactly
+    // n * (FU ? 3 : 1) store instructions per active lane -- d1 / d2 below, unconditional.  The dev
+    // ablations that skip or replace them (PCG_DEV_ABL_DEEP 2 / 3) therefore run single-buffered,
+    // with full waits, so their timings carry no fetch race.)
+#if defined(PCG_DEV_ABL_DEEP) && (PCG_DEV_ABL_DEEP == 2 || PCG_DEV_ABL_DEEP == 3)
+    const bool dbl = false;
+#else
     const bool dbl = PCG_STG_DB && !Ls<LP>::DB && (m >> 1) >= w.h && (64u / LP) * KS * J * (m >> 1) >= 64u;
+#endif
     uint32_t NB = 1;
     if (dbl) {
         m >>= 1;
@@ -1192,6 +1200,8 @@ PCG_DEV void ls_fgf_rootv(const Ls<LP>& c, GlSt d1, GlSt d2, const DBits& lb, co
             if (c.N != 0)
                 continue;
 #endif
+            // (exactly 1 + 2 * FU store instructions per output chunk: the wait_vm count above
+            // depends on it -- a conditional store here would let a round read stale LDS)
             d1.st(c2, y0);
             if constexpr (FU) {
                 const float4 y1 = OPC == OP_F ? f4_f(x[2], x[3]) : f4_g(x[2], x[3], lw[1], gs);
@@ -3173,6 +3183,12 @@ int sclls_layout(uint32_t N, uint32_t L, uint32_t lp, uint32_t vleaf, uint32_t* 
     const bool db = lp >= PCG_LS_DBITS_LP;
     if (L < 2 || L > 32 || N < 8)
         return -4;
+#if PCG_LS_INST
+    // a development build (tools/build_dev_lib.sh) rebuilt one list width with its knobs: plans of
+    // the other widths are refused at creation (PCG_E_UNSUPPORTED), not only at launch
+    if (lp != PCG_LS_INST)
+        return -4;
+#endif
     const uint32_t top = (uint32_t)__builtin_ctz(N);
     if (top > 3 + 12) // 5-bit slot fields for stages 3 .. top-1 in 64 bits
         return -4;

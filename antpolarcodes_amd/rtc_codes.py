@@ -93,6 +93,17 @@ def random_list_codes():
             j = next(g) % (i + 1)
             pos[i], pos[j] = pos[j], pos[i]
         out.append((N, L, sorted(pos[:nf])))
+    # longer codes: trees whose quarters (stage top-2) are recomputed from the channel inside the
+    # staged ops, with a fused / unfused child and both recomputed levels (own stream: the entries
+    # above keep their frozen sets and cache files)
+    g = _xorshift(0x5C1A12)
+    for N, L in ((512, 8), (1024, 8), (1024, 4)):
+        nf = N // 4 + next(g) % (N // 2)
+        pos = list(range(N))
+        for i in range(N - 1, 0, -1):
+            j = next(g) % (i + 1)
+            pos[i], pos[j] = pos[j], pos[i]
+        out.append((N, L, sorted(pos[:nf])))
     return out
 
 

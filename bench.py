@@ -85,14 +85,19 @@ def parse(argv=None):
                     help="also time the same steps with a second batch in flight (second plan and stream): "
                          "reported as roofline.throughput_2_in_flight_cw_per_s, never as value (off by default: "
                          "its overlapping launches would skew a profiler's per-launch average)")
-    ap.add_argument("--no-in-flight", dest="in_flight", action="store_false")
+    ap.add_argument("--no-in-flight", dest="single_stream", action="store_true",
+                    help="one batch at a time: no second-batch figure, and one stream for every mode (profiling "
+                         "and traffic runs: per-launch kernel statistics without overlapping launches)")
     ap.add_argument("--streams", type=int, default=0,
                     help="batches in flight: S plans on S HIP streams, step i on stream i %% S (default: 2 for "
                          "the adaptive modes, whose latency-bound list stage then overlaps the next batch's "
                          "Fast-SSC stage; 1 otherwise)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / reduction plumbing only: no GPU, no decode (CPU tests)")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    if a.single_stream:
+        a.in_flight = False
+    return a
 
 
 # --------------------------------------------------------------------------- launcher
@@ -438,7 +443,7 @@ def main(argv=None):
             d_ref = torch.from_numpy(info_h).to(dev)
         # S batches in flight (--streams): one plan, output buffers and HIP stream each; every
         # step decodes the whole resident batch on stream i % S
-        S = args.streams if args.streams > 0 else (2 if adaptive else 1)
+        S = args.streams if args.streams > 0 else (2 if adaptive and not args.single_stream else 1)
         plans = [Plan(N, L, frozen, systematic=True, crc=crc, device=local, adaptive=adaptive, fixed=fixed)
                  for _ in range(S)]
         for q in plans:
@@ -556,6 +561,9 @@ def main(argv=None):
                        "parallelism": f"{world} independent shard(s), no collective",
                        "streams": S},
             "roofline": roof,
+            **({"value_scope": f"{S} batches in flight on {S} HIP streams (plans), step i on stream i % {S}: the "
+                               "wall-time throughput of overlapping batches -- not comparable with a one-stream "
+                               "value (--no-in-flight / --streams 1)"} if S > 1 else {}),
             "src_digest": digest,
         }
         # developer environment switches that changed the plan (pcg_plan_desc.dev_overrides):

@@ -110,9 +110,9 @@ public:
 /// Output container of the GPU float decoders (outputContainer()): after a Fast-SSC float
 /// decode (N <= 16384) it holds the soft codeword word for word (FloatContainer::getSoftBits
 /// of the reference); otherwise the decoded codeword's hard decisions as sign bits
-/// (+0.0 / -0.0) -- getPackedBits / getFloatBits / getPackedInformationBits exact -- and
-/// the soft accessors raise std::logic_error (the list, 8-bit and adaptive kernels keep
-/// hard decisions only).
+/// (+0.0 / -0.0) -- getPackedBits / getFloatBits / getPackedInformationBits exact -- which
+/// the soft accessors return: the selected path's signed hard decisions, whose signs are the
+/// reference's (only the signs of its list decoders' bit floats are observable).
 class DecodedFloatContainer : public FloatContainer
 {
     bool mSoft = false;
@@ -126,7 +126,7 @@ public:
 };
 
 /// Output container of the GPU 8-bit decoders: hard decisions as char bits (0 -> 127,
-/// 1 -> -128, CharContainer::insertPackedBits); soft accessors raise std::logic_error.
+/// 1 -> -128, CharContainer::insertPackedBits), which the soft accessors return.
 class DecodedCharContainer : public CharContainer
 {
 public:

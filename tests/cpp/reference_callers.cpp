@@ -285,6 +285,19 @@ static int run_gpu(int argc, char** argv)
             packed_signs(mDecoder->outputContainer(), N, cw.data());
             std::printf(" ");
             hex(cw.data(), N / 8);
+            // getSoftCodeword (decoder.cpp:147): the reference's soft codeword (Fast-SSC float) or
+            // the selected path's signed hard decisions (list / adaptive decoders); its signs
+            // (AdaptiveMixed's container is its 8-bit stage's CharContainer when that stage succeeded,
+            // as in the reference: char bits then)
+            const bool chars = dynamic_cast<CharContainer*>(mDecoder->outputContainer()) != nullptr;
+            std::vector<float> sw(N);
+            mDecoder->getSoftCodeword(sw.data());
+            const signed char* sb = reinterpret_cast<const signed char*>(sw.data());
+            std::vector<unsigned char> sc(N / 8, 0);
+            for (size_t i = 0; i < N; ++i)
+                sc[i / 8] |= (unsigned char)(((chars ? sb[i] < 0 : std::signbit(sw[i])) ? 1u : 0u) << (7 - i % 8));
+            std::printf(" ");
+            hex(sc.data(), N / 8);
             std::printf("\n");
         }
     }
@@ -297,13 +310,18 @@ static int run_gpu(int argc, char** argv)
     packed_signs(decs[0]->outputContainer(), N, cw.data());
     for (size_t i = 0; i < N; ++i)
         CHECK(((cw[i / 8] >> (7 - i % 8)) & 1u) == (std::signbit(soft[i]) ? 1u : 0u));
-    bool threw = false;
-    try {
-        decs[3]->getSoftCodeword(soft.data()); // SCL keeps hard decisions only
-    } catch (const std::logic_error&) {
-        threw = true;
-    }
-    CHECK(threw);
+    // SclAvxFloat: getSoftInformation = the soft codeword at the information positions
+    std::vector<float> si(N - frozen.size());
+    decs[3]->setSignal(llr);
+    decs[3]->decode();
+    decs[3]->getSoftCodeword(soft.data());
+    decs[3]->getSoftInformation(si.data());
+    std::vector<char> isfz(N, 0);
+    for (unsigned f : frozen)
+        isfz[f] = 1;
+    for (size_t i = 0, j = 0; i < N; ++i)
+        if (!isfz[i])
+            CHECK(std::memcmp(&soft[i], &si[j++], sizeof(float)) == 0);
     std::printf("gpu ok\n");
     return 0;
 }

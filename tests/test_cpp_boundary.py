@@ -96,7 +96,8 @@ def test_simulator_encoder_sequence_small_codes(tmp_path, oracle):
 def test_simulator_decoder_sequence_on_gpu(tmp_path, oracle):
     """setCoders' decoders (FastSscAvxFloat, AdaptiveFloat, AdaptiveMixed, SclAvxFloat by their
     reference names) through setSignal -> decode -> packedOutput, one frame at a time, equal the
-    oracle; outputContainer() holds the decoded codeword."""
+    oracle; outputContainer() holds the decoded codeword and getSoftCodeword's signs are the
+    selected path's codeword (the reference's mBitContainer, scl_avx_float.cpp:711-750)."""
     from antpolarcodes_amd import frames
     exe = build(tmp_path, "reference_callers")
     fr = oracle.frozen_bits_bb(1024, 512, 0.0)
@@ -125,8 +126,11 @@ def test_simulator_decoder_sequence_on_gpu(tmp_path, oracle):
     for line in r.stdout.splitlines():
         if line.endswith("ok"):
             continue
-        k, f, okv, info, cw = line.split()
+        k, f, okv, info, cw, soft = line.split()
         k, f = int(k), int(f)
         assert int(okv) == int(exp[k][1][f]), (k, f)
         assert np.array_equal(np.frombuffer(bytes.fromhex(info), np.uint8), exp[k][0][f]), (k, f)
         assert np.array_equal(np.frombuffer(bytes.fromhex(cw), np.uint8), np.asarray(enc[k])[f]), (k, f)
+        # getSoftCodeword's signs: the selected path's codeword (systematic: the encoding of the
+        # decoded information), for the soft Fast-SSC codeword and the list / adaptive decoders alike
+        assert np.array_equal(np.frombuffer(bytes.fromhex(soft), np.uint8), np.asarray(enc[k])[f]), (k, f)

@@ -20,15 +20,17 @@ def code(oracle):
     return N, fr, llr
 
 
-@pytest.mark.parametrize("mode", ["0", "1", "2", "3"])
+@pytest.mark.parametrize("mode", ["0", "1", "2", "2p", "3"])
 def test_host_pipeline_three_chunks_scl(oracle, monkeypatch, code, mode):
     """SCL-8 over 3000 frames in chunks of 1024 (three chunks, the last one partial): info, ok
-    and metrics bit-exact against the oracle, in every staging mode; then a second call on the
-    same plan (slots reused) and a pinned caller buffer (copied from directly)."""
+    and metrics bit-exact against the oracle, in every staging mode (2p: staged and copied in
+    1 MB pieces, the last one partial); then a second call on the same plan (slots reused) and
+    a pinned caller buffer (copied from directly)."""
     import torch
     from antpolarcodes_amd._native import Plan
     N, fr, llr = code
-    monkeypatch.setenv("PCG_HOST_PIPE", mode)
+    monkeypatch.setenv("PCG_HOST_PIPE", mode[0])
+    monkeypatch.setenv("PCG_HOST_PIECE_MB", "1" if mode == "2p" else "0")
     monkeypatch.setenv("PCG_HOST_CHUNK", "1024")
     oi, ook, om, _, _ = oracle.scl_decode(N, 8, fr, llr, crc=8, paths=True)
     p = Plan(N, 8, fr, crc=8, device=0)
@@ -51,6 +53,7 @@ def test_host_pipeline_sc_and_int8(oracle, monkeypatch, code, mode):
     N, fr, llr = code
     monkeypatch.setenv("PCG_HOST_PIPE", mode)
     monkeypatch.setenv("PCG_HOST_CHUNK", "448")
+    monkeypatch.setenv("PCG_HOST_PIECE_MB", "1")  # (448 frames = 1.75 MB: two pieces per chunk)
     p = Plan(N, 1, fr, crc=8, device=0)
     gi, gok, _ = p.decode_host(llr)
     oi, ook = oracle.sc_decode(N, fr, llr, crc=8)

@@ -124,10 +124,41 @@ def test_soft_information_and_unsupported(oracle):
     sc = d.getSoftCodeword()
     info_pos = np.setdiff1d(np.arange(N), fr)
     assert np.array_equal(d.getSoftInformation().view(np.uint32), sc[info_pos].view(np.uint32))
-    scl = pypolar.PolarDecoder(N, 8, fr, "gpu")
-    scl.decode_vector(sig)
-    with pytest.raises(Exception, match="soft"):
-        scl.getSoftCodeword()
+
+
+
+def test_soft_outputs_of_list_char_and_adaptive_decoders(oracle):
+    """List, 8-bit and adaptive GPU decoders return the selected path's signed hard decisions
+    from getSoftCodeword / getSoftInformation (the reference copies the selected path's bit
+    buffer into mBitContainer, scl_avx_float.cpp:711-750, and returns it, decoder.cpp:147-151;
+    only its signs are observable): signs = the oracle's selected-path codeword, the soft
+    information = the codeword at the information positions."""
+    from antpolarcodes_amd import frames, pypolar
+    N, K = 256, 128
+    fr = oracle.frozen_bits_bb(N, K, 0.0)
+    info_pos = np.setdiff1d(np.arange(N), fr)
+    llr, _, _ = frames.awgn_frames(N, fr, 12, 1.0, seed=3, crc=8)
+    x8 = np.clip(np.rint(llr * 10.0), -128, 127).astype(np.int8)
+    cases = [("gpu", 8, llr, oracle.scl_decode(N, 8, fr, llr, crc=8, carry=True)[0]),
+             ("char", 8, x8, oracle.sclc_decode(N, 8, fr, x8, crc=8, carry=True)[0]),
+             ("char", 1, x8, oracle.scc_decode(N, fr, x8, crc=8)[0])]
+    sc_i, sc_k = oracle.sc_decode(N, fr, llr, crc=8)
+    scl_i = oracle.scl_decode(N, 8, fr, llr, crc=8)[0]
+    ad = sc_i.copy()
+    ad[sc_k == 0] = scl_i[sc_k == 0]
+    cases.append(("mixed", 8, llr, ad))
+    for typ, L, x, exp_info in cases:
+        d = pypolar.PolarDecoder(N, L, fr, typ)
+        d.setErrorDetection(8)
+        exp_cw = np.asarray(oracle.encode(N, fr, exp_info, systematic=True, crc=0))
+        for f in range(x.shape[0]):
+            assert np.array_equal(d.decode_vector(x[f]), exp_info[f]), (typ, L, f)
+            soft = d.getSoftCodeword()
+            assert soft.shape == (N,)
+            neg = soft < 0 if soft.dtype == np.int8 else np.signbit(soft)
+            assert np.array_equal(np.packbits(neg.astype(np.uint8)), exp_cw[f]), (typ, L, f)
+            si = d.getSoftInformation()
+            assert np.array_equal(si.view(np.uint8), soft[info_pos].view(np.uint8)), (typ, L, f)
 
 
 def test_scl_metric_carry_q8_fixture(oracle):

@@ -125,17 +125,26 @@ def test_destroy_during_compile_and_shared_compile(tmp_path):
     assert len(list((tmp_path / "b").glob("pcg_*.co"))) == 1
 
 
+# catalogue entries whose frozen sets the Fast-SSC classifier rejects (PCG_E_FROZEN, as the
+# reference's createDecoder throws): listed so that a code that stops constructing fails the test
+_REJECTED_CATALOGUE_ENTRIES = 2
+
+
 def test_shipped_cache_holds_the_catalogue():
     """The build (antpolarcodes_amd/rtc_warm.py) ships the specialised kernels of the whole
     catalogue (antpolarcodes_amd/rtc_codes.py: the benchmark configurations and the validation
     codes the GPU tests use) next to the library, with the hiprtc version they were built by:
-    they load without any compile."""
+    every code that constructs has its file there, under the name a lookup reads, and loads
+    without any compile."""
     import os
     from antpolarcodes_amd import rtc_warm
+    from antpolarcodes_amd.rtc_codes import codes
     assert os.path.isfile(os.path.join(rtc_warm.CACHE, "HIPRTC_VERSION"))
     code = ("from antpolarcodes_amd.rtc_codes import codes\n"
             "from antpolarcodes_amd._native import PcgError\n"
-            "n = 0\n"
+            "from antpolarcodes_amd import rtc_warm\n"
+            "n, rej, missing = 0, 0, []\n"
+            "b = ctypes.create_string_buffer(256)\n"
             "for N, L, (kind, arg), crc, sysm, *ad in codes():\n"
             "    fr = list(arg) if kind == 'set' else frozen_bits(N, arg, 0.0, kind)\n"
             "    try:\n"
@@ -143,12 +152,55 @@ def test_shipped_cache_holds_the_catalogue():
             "                 adaptive=ad[:1] in (['adaptive'], ['adaptive_char']),\n"
             "                 fixed=ad[:1] in (['char'], ['adaptive_char']))\n"
             "    except PcgError:\n"
+            "        rej += 1\n"
             "        continue\n"
+            "    assert lib().pcg_dev_rtc_lookup_name(p._h, rtc_warm.CACHE.encode(), b, 256) == 0\n"
+            "    missing += [f for f in b.value.decode().split() if not os.path.isfile(os.path.join(rtc_warm.CACHE, f))]\n"
             "    p.specialize()\n"
             "    n += 1\n"
-            "print('codes', n, 'compiles', lib().pcg_dev_rtc_compiles())\n")
-    out = _run(code, {"PCG_RTC_CACHE": "0"}, timeout=300)
+            "print('codes', n, 'rejected', rej, 'missing', missing, 'compiles', lib().pcg_dev_rtc_compiles())\n")
+    out = _run("import os\n" + code, {"PCG_RTC_CACHE": "0"}, timeout=300)
     assert "compiles 0" in out, out
+    assert "missing []" in out, out
+    assert "codes %d rejected %d " % (len(codes()) - _REJECTED_CATALOGUE_ENTRIES, _REJECTED_CATALOGUE_ENTRIES) in out, out
+
+
+def test_warm_names_follow_the_cache_version(tmp_path):
+    """A cache directory recorded under another hiprtc version (a build machine whose compiler
+    changed): rtc_warm rewrites its HIPRTC_VERSION to the running version, so the files it writes
+    are named exactly as a lookup in that directory reads them, and prunes the stale entries."""
+    from antpolarcodes_amd import rtc_warm
+    d = tmp_path / "shipped"
+    d.mkdir()
+    (d / "HIPRTC_VERSION").write_text("0.0\n")
+    (d / "pcg_0000000000000000.co").write_bytes(b"stale")
+    code = (16, 1, ("BB", 8), 0, False)
+    keep = rtc_warm.warm(quiet=True, cache=str(d), todo=[code])
+    assert (d / "HIPRTC_VERSION").read_text().strip() == rtc_warm.hiprtc_version() != "0.0"
+    assert len(keep) == 1 and sorted(f.name for f in d.glob("*.co")) == sorted(keep)
+    _, rc, err, written, lookups = rtc_warm._one(code, str(d))
+    assert rc == 0 and written == lookups == sorted(keep), err
+
+
+def test_exit_wait_bound_keeps_a_failure_status(tmp_path):
+    """PCG_RTC_EXIT_WAIT: a process leaving while a compile still runs never reports success
+    (the status it asked for is replaced by PCG_RTC_EXIT_STATUS, 75)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prog = ("import sys; sys.path.insert(0, %r)\n"
+            "from antpolarcodes_amd._native import Plan\n"
+            "from antpolarcodes_amd.construction import frozen_bits\n"
+            "p = Plan(64, 1, frozen_bits(64, 20, 0.0, 'BB'), systematic=False, crc=32, device=-1)\n"
+            "p.specialize(wait=False)\n" % root)
+    env = {k: v for k, v in os.environ.items() if not k.startswith("PCG_")}
+    env.update({"PCG_RTC_CACHE": str(tmp_path), "PCG_RTC_EXIT_WAIT": "0"})
+    r = subprocess.run([sys.executable, "-c", prog], env=env, capture_output=True, text=True, timeout=300)
+    if r.returncode == 0:  # the compile finished before exit: nothing was cut short
+        assert "still running" not in r.stderr
+        return
+    assert r.returncode == 75 and "still running" in r.stderr, (r.returncode, r.stderr[-2000:])
 
 
 def test_dev_build_knobs_reach_the_specialised_source():

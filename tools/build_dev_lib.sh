@@ -5,7 +5,8 @@
 # (SKIP_MAKE: the in-tree objects are current; lets several variants build in parallel)
 # sclls_kernel.hip: the variant is one list width (LP, default 8) plus the host part, replacing
 # the objects sclls_kernel.hip.o and sclls_lp<LP>.o; its specialised (hiprtc) kernels carry the
-# same -D knobs (sclls_rtc_defines).
+# same -D knobs (sclls_rtc_defines).  Plans of the other list widths are refused by such a library
+# (PCG_E_UNSUPPORTED at creation: their objects were built with the default knobs).
 set -e
 TAG=$1; SRC=$2; shift 2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
