@@ -454,12 +454,14 @@ const char* pcg_last_error(void) { return g_last_error.c_str(); }
 // Development aid, not part of include/pcg.h: with PCG_OPPROF=1 in the environment
 // the kernels accumulate s_memtime cycles and counts per op code; this copies the
 // 64 x {cycles, count} table out and clears it.
-// (pcg_dev_opprof_fetch_n: the first n <= 256 entries -- the list kernel's profiler keeps
-// requested global read / write bytes per op bucket in entries 64-127 / 128-191.)
+// (pcg_dev_opprof_fetch_n: the first n <= kProfN entries -- the list kernel's profiler keeps
+// requested global read / write bytes per op bucket in entries 64-127 / 128-191, and a
+// -DPCG_LS_PROF_POS build the cycles of schedule position k in entry 256 + k.)
+constexpr int kProfN = 4096;
 int pcg_dev_opprof_fetch_n(unsigned long long* out, int n)
 {
-    if (n < 0 || n > 256)
-        return fail(PCG_E_ARG, "opprof: n > 256");
+    if (n < 0 || n > kProfN)
+        return fail(PCG_E_ARG, "opprof: n > 4096");
     if (!g_prof) {
         std::memset(out, 0, (size_t)n * sizeof(unsigned long long));
         return PCG_OK;
@@ -467,7 +469,7 @@ int pcg_dev_opprof_fetch_n(unsigned long long* out, int n)
     if (hipDeviceSynchronize() != hipSuccess ||
         hipMemcpy(out, g_prof, (size_t)n * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
         return fail(PCG_E_HIP, "opprof copy failed");
-    (void)hipMemset(g_prof, 0, 256 * sizeof(unsigned long long));
+    (void)hipMemset(g_prof, 0, kProfN * sizeof(unsigned long long));
     return PCG_OK;
 }
 int pcg_dev_opprof_fetch(unsigned long long* out128) { return pcg_dev_opprof_fetch_n(out128, 128); }
@@ -513,6 +515,18 @@ int pcg_dev_rtc_version(char* out, size_t n)
         return fail(PCG_E_ARG, "null argument");
     snprintf(out, n, "%s", pcg::rtc_version().c_str());
     return PCG_OK;
+}
+
+// Development aid, not part of include/pcg.h: the plan's flattened op schedule (n words at most;
+// returns the count) -- tools/ls_prof_pos.py names the per-position cycles with it.
+int pcg_dev_plan_ops(const pcg_plan* p, uint32_t* out, int n)
+{
+    if (!p || !out || n < 0)
+        return fail(PCG_E_ARG, "null argument");
+    const auto& ops = p->host.ops;
+    for (int k = 0; k < n && k < (int)ops.size(); ++k)
+        out[k] = ops[k];
+    return (int)ops.size();
 }
 
 // Development aid, not part of include/pcg.h: hiprtc compiles this process started.
@@ -1012,8 +1026,8 @@ static int decode_impl(pcg_plan* p,
     a.llr8 = llr8;
     a.metric0 = p->metric0;
     if (p->dev_opprof) {
-        if (!g_prof && hipMalloc(&g_prof, 256 * sizeof(unsigned long long)) == hipSuccess)
-            (void)hipMemset(g_prof, 0, 256 * sizeof(unsigned long long));
+        if (!g_prof && hipMalloc(&g_prof, kProfN * sizeof(unsigned long long)) == hipSuccess)
+            (void)hipMemset(g_prof, 0, kProfN * sizeof(unsigned long long));
         a.prof = g_prof;
     }
     a.flags = p->dev_flags;

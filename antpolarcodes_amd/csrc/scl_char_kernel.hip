@@ -615,6 +615,10 @@ PCG_DEV void sclc_body(const KernelArgs& a, uint32_t Sl)
             wsync();
             if (code <= OP_COMB || code == OP_CS_R0)
                 SC_ADD(a.prof, code & 63u, to0);
+#if defined(PCG_SCLC_PROF) && defined(PCG_SCLC_PROF_POS) // dev: cycles per schedule position
+            if (a.prof && w.lane == 0 && k < 3840u)
+                atomicAdd(&a.prof[256u + k], (unsigned long long)(__builtin_amdgcn_s_memtime() - to0));
+#endif
         }
         SC_T0(tx0);
         // extractBestPath (scl_fip_char.cpp:816-856): first path in list order whose

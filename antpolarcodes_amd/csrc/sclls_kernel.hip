@@ -2982,6 +2982,9 @@ PCG_DEV void sclls_body(const KernelArgs& a)
         ls_walk<LP, 0>(c, P);
 #else
         for (uint32_t kop = 0; kop < a.nops; ++kop) {
+#ifdef PCG_LS_PROF
+            const uint32_t kop0 = kop;
+#endif
             const uint32_t w = ld_const(a.ops, kop);
             const uint32_t code = op_code(w), s = op_stage(w), o = op_off(w);
 #ifdef PCG_LS_PROF
@@ -3013,6 +3016,10 @@ PCG_DEV void sclls_body(const KernelArgs& a)
                     lprof[b] += t1 - t0;
                     lprof[64 + b] += ls_gb_ctr()[0];
                     lprof[128 + b] += ls_gb_ctr()[1];
+#ifdef PCG_LS_PROF_POS // dev: the cycles of every schedule position (tools/ls_prof_pos.py)
+                    if (a.prof && kop0 < 3840u)
+                        atomicAdd(&a.prof[256u + kop0], (unsigned long long)(t1 - t0));
+#endif
                 }
             }
 #endif

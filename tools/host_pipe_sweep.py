@@ -2,7 +2,9 @@
 threads and chunk sizes (capi.cpp decode_host; the variables are read per call), for a
 resident numpy batch of config 3 (SCL-8, N=1024, 2^16 frames) -- and from a page-locked
 caller buffer, which the pipeline copies from directly.
-    python tools/host_pipe_sweep.py [mode: scl8|sc]"""
+    python tools/host_pipe_sweep.py [mode: scl8|sc] [pieces]
+`pieces`: only the pinned-staging mode over staging piece sizes (PCG_HOST_PIECE_MB), staging
+threads and chunk sizes."""
 import os
 import sys
 import time
@@ -63,6 +65,15 @@ d.copy_(pinned, non_blocking=True)
 torch.cuda.synchronize()
 print(f"H2D of the batch (torch, pinned) {llr.nbytes / (time.perf_counter() - t0) / 1e9:.1f} GB/s")
 print(f"serial (PCG_HOST_PIPE=0) {rate(llr, PCG_HOST_PIPE=0):.4g} cw/s")
+if "pieces" in sys.argv[1:]:
+    for chunk in (16384, 32768):
+        print(f"page-locked caller buffer, chunk {chunk}: {rate(pinned.numpy(), PCG_HOST_CHUNK=chunk):.4g} cw/s")
+    for thr in (8, 12, 16):
+        for chunk in (16384, 32768):
+            for pmb in (0, 2, 4, 8, 16):
+                r = rate(llr, PCG_HOST_PIPE=2, PCG_HOST_THREADS=thr, PCG_HOST_CHUNK=chunk, PCG_HOST_PIECE_MB=pmb)
+                print(f"pinned staging (2), {thr} threads, chunk {chunk}, piece {pmb} MB: {r:.4g} cw/s", flush=True)
+    sys.exit(0)
 for chunk in (16384, 32768):
     print(f"pageable runtime copies (1), chunk {chunk}: {rate(llr, PCG_HOST_PIPE=1, PCG_HOST_CHUNK=chunk):.4g} cw/s")
 for thr in (8, 16):
