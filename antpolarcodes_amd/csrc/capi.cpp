@@ -1338,8 +1338,11 @@ static int decode_host(pcg_plan* p, const void* llr, size_t elem, uint64_t F, ui
     const bool reg = mode == 3 && !direct;
     const int threads = env_int("PCG_HOST_THREADS", 8);
     const bool nt = env_int("PCG_HOST_NT", 1) != 0;
-    // staging piece (PCG_HOST_PIECE_MB, default 8 MB; 0: the whole chunk at once, round 5)
-    const int piece_mb = env_int("PCG_HOST_PIECE_MB", 8);
+    // staging piece (PCG_HOST_PIECE_MB, default 16 MB; 0: the whole chunk at once, round 5).
+    // Measured on config 3 (profiles/r06d_host_pieces.txt, 8 threads, chunk 16384 frames = 64 MB):
+    // whole chunk 1.008e7 cw/s, pieces of 4 / 8 / 16 MB 1.029e7 / 1.068e7 / 1.079e7 (a page-locked
+    // caller buffer, no staging: 1.127e7)
+    const int piece_mb = env_int("PCG_HOST_PIECE_MB", 16);
     const size_t piece = piece_mb > 0 ? (size_t)piece_mb << 20 : ~size_t(0);
     int rc = pipe_alloc(p, chunk, fb, stage);
     if (rc != 0)

@@ -204,6 +204,127 @@ PCG_DEV void op_fg(Wave<LP, I8>& w, bool g, uint32_t s, uint32_t o, bool act)
     w.own(cs);
 }
 
+// ---- F / G with more lanes than paths (round 6) ------------------------------------------
+// While fewer than LP paths exist (every codeword until its first branching leaf: P = 1), the
+// idle lanes of a codeword group share the units of the active paths' F / G: lanes p = path
+// (mod pp), pp = P rounded up to a power of two, each compute a contiguous share of the path's
+// output units and write them into the path's own column (its slot table and bit row are read
+// through the path's lane).  Same bytes as op_fg, fewer serial units per lane.
+#ifndef PCG_SCLC_SHARE
+#define PCG_SCLC_SHARE 1
+#endif
+#ifndef PCG_SCLC_ROOTL
+#define PCG_SCLC_ROOTL 1
+#endif
+// waves per SIMD the register allocation must allow (<= 128 VGPRs: the 14 waves per CU that the
+// 12 KB LDS budget gives)
+#ifndef PCG_SCLC_MINW
+#define PCG_SCLC_MINW 4
+#endif
+template <int LP, bool I8>
+PCG_DEV void op_fg_shared(Wave<LP, I8>& w, bool g, uint32_t s, uint32_t o, uint32_t P)
+{
+    const uint32_t cs = s - 1, hq = 1u << (cs - 4); // output units (h = 2^cs >= 32 bytes)
+    uint32_t pp = 1;
+    while (pp < P)
+        pp <<= 1;
+    uint32_t hs = LP / pp; // lanes per path, each with an even number of units
+    while (hs > 1 && 2u * hs > hq)
+        hs >>= 1;
+    const uint32_t path = w.p & (pp - 1), i = w.p / pp, dl = w.gb | path;
+    const uint64_t pptr = __shfl(w.ptr, (int)dl, 64);
+    const uint32_t* prow = w.lds + w.ly.bits + dl;   // the path's bit row, word q at [q * 64]
+    const uint32_t n = hq / hs, c0 = n * i;          // this lane's units [c0, c0 + n)
+    const bool act = path < P && i < hs;
+    if (act) {
+        const uint32_t sl = w.gb | (uint32_t)((pptr >> (5u * s)) & 31u);
+        auto run = [&](const auto& src, const auto& dst) {
+#pragma unroll 1
+            for (uint32_t c = c0; c < c0 + n; c += 2) { // (n even: hq >= 2 hs)
+                const uint4 a0 = src.ld(c), b0 = src.ld(c + hq), a1 = src.ld(c + 1), b1 = src.ld(c + 1 + hq);
+                if (g) {
+                    const uint32_t p0 = o + 16u * c, bb = prow[(p0 >> 5) << 6] >> (p0 & 31u);
+                    dst.st(c, g16(a0, b0, bb & 0xffffu));
+                    dst.st(c + 1, g16(a1, b1, bb >> 16));
+                } else {
+                    dst.st(c, f16(a0, b0));
+                    dst.st(c + 1, f16(a1, b1));
+                }
+            }
+        };
+        auto with_dst = [&](const auto& src) {
+            if (cs < w.ly.Sl)
+                run(src, LdsDst{ w.lds_stage(cs), dl });
+            else
+                run(src, GlbDst{ w.glb_stage(cs), dl });
+        };
+        if (s == w.ly.mt)
+            with_dst(RootSrc<I8>{ ChanSrc<I8>{ w.chan, w.N }, prow, w.right ? 1u : 0u });
+        else if (s < w.ly.Sl)
+            with_dst(LdsSrc{ w.lds_stage(s), sl });
+        else
+            with_dst(GlbSrc{ w.glb_stage(s), sl });
+    }
+    w.own(cs);
+}
+
+// The left child of the root (stage top-1, F(y_j, y_j+N/2): the same bytes for every path) read
+// by an F / G with every lane busy (the G of the root's left child, after its left subtree): the
+// LP lanes of a codeword compute its units once between them -- unit u by lane u mod LP -- and each
+// path reads the two units of an output from their lane (ds_bpermute), instead of every path
+// recomputing all of them (two channel loads and an F per unit).
+template <int LP, bool I8, int SLOTS>
+PCG_DEV void op_fg_rootl_slots(Wave<LP, I8>& w, bool g, uint32_t o, uint32_t hq, bool act)
+{
+    // unit u of the child (2 hq = 2 SLOTS LP units) is computed by lane u mod LP as its u[u / LP]
+    const RootSrc<I8> rs{ ChanSrc<I8>{ w.chan, w.N }, w.row(), 0u };
+    uint4 u[2 * SLOTS];
+#pragma unroll
+    for (int k = 0; k < 2 * SLOTS; ++k)
+        u[k] = rs.ld((uint32_t)k * LP + w.p);
+    const uint32_t cs = w.ly.mt - 1;
+    auto run = [&](const auto& dst) {
+#pragma unroll
+        for (int k = 0; k < SLOTS; ++k) {
+#pragma unroll 1 // (one output unit at a time: the kernel stays at 4 waves per SIMD)
+            for (uint32_t q = 0; q < (uint32_t)LP; ++q) {
+                const int sl = (int)(w.gb | q);
+                const uint32_t c = (uint32_t)k * LP + q; // output unit: a = unit c, b = unit c + hq
+                const uint4 a = make_uint4(__shfl(u[k].x, sl, 64), __shfl(u[k].y, sl, 64), __shfl(u[k].z, sl, 64),
+                                           __shfl(u[k].w, sl, 64));
+                const uint4 b = make_uint4(__shfl(u[k + SLOTS].x, sl, 64), __shfl(u[k + SLOTS].y, sl, 64),
+                                           __shfl(u[k + SLOTS].z, sl, 64), __shfl(u[k + SLOTS].w, sl, 64));
+                if (!act)
+                    continue;
+                if (g)
+                    dst.st(c, g16(a, b, w.bits_at(o + 16u * c, 16)));
+                else
+                    dst.st(c, f16(a, b));
+            }
+        }
+    };
+    if (cs < w.ly.Sl)
+        run(LdsDst{ w.lds_stage(cs), w.lane });
+    else
+        run(GlbDst{ w.glb_stage(cs), w.lane });
+    (void)hq;
+}
+template <int LP, bool I8>
+PCG_DEV bool op_fg_rootl(Wave<LP, I8>& w, bool g, uint32_t s, uint32_t o, bool act)
+{
+    if (!PCG_SCLC_ROOTL || s < 6u || s != w.ly.mt || w.right || s == w.top)
+        return false;
+    const uint32_t hq = 1u << (s - 5); // output units (s >= 6); the child has 2 hq units
+    if (hq < (uint32_t)LP || 2u * hq > 4u * LP)
+        return false;
+    if (hq == (uint32_t)LP)
+        op_fg_rootl_slots<LP, I8, 1>(w, g, o, hq, act);
+    else
+        op_fg_rootl_slots<LP, I8, 2>(w, g, o, hq, act);
+    w.own(s - 1);
+    return true;
+}
+
 // CombineBits (fip_char.h:165-201) on sign bits: bit[o+i] ^= bit[o+h+i]
 template <int LP, bool I8>
 PCG_DEV void op_comb(Wave<LP, I8>& w, uint32_t s, uint32_t o, bool act)
@@ -563,10 +684,12 @@ PCG_DEV void sclc_body(const KernelArgs& a, uint32_t Sl)
             SC_T0(to0);
             switch (code) {
             case OP_F:
-                op_fg(w, false, s, o, act);
-                break;
             case OP_G:
-                op_fg(w, true, s, o, act);
+                // (wave-uniform choices: P and the stage are the same for every codeword)
+                if (PCG_SCLC_SHARE && 2u * P <= (uint32_t)LP && s != w.top && s >= 6u)
+                    op_fg_shared(w, code == OP_G, s, o, P);
+                else if (!op_fg_rootl(w, code == OP_G, s, o, act))
+                    op_fg(w, code == OP_G, s, o, act);
                 break;
             case OP_COMB:
                 op_comb(w, s, o, act);
@@ -694,12 +817,15 @@ PCG_DEV void sclc_rtc(const KernelArgs& a)
 }
 } // namespace
 
-extern "C" __global__ void __launch_bounds__(64) scl_char_rtc_kernel(KernelArgs a) { sclc_rtc<true>(a); }
-extern "C" __global__ void __launch_bounds__(64) scl_char_rtc_kernel_f32(KernelArgs a) { sclc_rtc<false>(a); }
+extern "C" __global__ void __launch_bounds__(64, PCG_SCLC_MINW) scl_char_rtc_kernel(KernelArgs a) { sclc_rtc<true>(a); }
+extern "C" __global__ void __launch_bounds__(64, PCG_SCLC_MINW) scl_char_rtc_kernel_f32(KernelArgs a)
+{
+    sclc_rtc<false>(a);
+}
 
 #else
 template <int LP, bool I8>
-__global__ void __launch_bounds__(64) scl_char_kernel(KernelArgs a, uint32_t Sl)
+__global__ void __launch_bounds__(64, PCG_SCLC_MINW) scl_char_kernel(KernelArgs a, uint32_t Sl)
 {
     sclc_body<LP, I8>(a, Sl);
 }

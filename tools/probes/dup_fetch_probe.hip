@@ -11,6 +11,11 @@
 //   2  src(l) = (l & ~7) | perm[l & 7]     (8-lane groups, 4 distinct slots, scattered lanes)
 //   3  src(l) = l & ~7                     (every 8-lane group reads one slot)
 // Run each pattern under `rocprofv3 --pmc FETCH_SIZE`; compare with the unique bytes printed.
+// Measured (profiles/r06d_dup_fetch_probe.txt): all four patterns fetch the same 537 MB per
+// launch (FETCH_SIZE x 2, the gfx950 correction) = 8 lines x 128 B per instruction -- fetches are
+// per 128-B line and instruction.  In the slab layout the 8 path columns of a codeword group for
+// one chunk ARE one 128-B line, so a G reading any mix of slots fetches exactly that line: there
+// are no duplicate slot reads to remove.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
