@@ -154,78 +154,54 @@ struct Wave {
     }
 };
 
-// F / G of the node at stage s (n = 2^s) into stage s-1.  Large nodes (2^(s-1) >= 16 bytes):
-// output units [c0, c0 + nu) of the path whose stage-s slot lane is sl, written into column dl,
-// G bits / the recomputed right root child from the bit row rowp -- the own lane's everything for
-// a lane on its own path, the path's lane's for lanes sharing it (op_fg_shared).  Small nodes:
-// the own lane.
-template <int LP, bool I8>
-PCG_DEV void op_fg_at(Wave<LP, I8>& w, bool g, uint32_t s, uint32_t o, bool act, uint32_t sl, uint32_t dl,
-                      const uint32_t* rowp, uint32_t c0, uint32_t nu)
-{
-    const uint32_t cs = s - 1, h = 1u << cs;
-    if (act && h >= 16) {
-        auto run = [&](const auto& src, const auto& dst) {
-            const uint32_t hq = h >> 4;
-            uint32_t c = c0;
-            for (; c + 2 <= c0 + nu; c += 2) { // two units in flight
-                const uint4 a0 = src.ld(c), b0 = src.ld(c + hq), a1 = src.ld(c + 1), b1 = src.ld(c + 1 + hq);
-                if (g) {
-                    const uint32_t p0 = o + 16u * c, bb = rowp[(p0 >> 5) << 6] >> (p0 & 31u);
-                    dst.st(c, g16(a0, b0, bb & 0xffffu));
-                    dst.st(c + 1, g16(a1, b1, bb >> 16));
-                } else {
-                    dst.st(c, f16(a0, b0));
-                    dst.st(c + 1, f16(a1, b1));
-                }
-            }
-            if (c < c0 + nu) { // hq == 1
-                const uint4 a = src.ld(c), b = src.ld(c + hq);
-                const uint32_t p0 = o + 16u * c;
-                dst.st(c, g ? g16(a, b, (rowp[(p0 >> 5) << 6] >> (p0 & 31u)) & 0xffffu) : f16(a, b));
-            }
-        };
-        auto with_dst = [&](const auto& src) {
-            if (cs < w.ly.Sl)
-                run(src, LdsDst{ w.lds_stage(cs), dl });
-            else
-                run(src, GlbDst{ w.glb_stage(cs), dl });
-        };
-        if (s == w.ly.mt)
-            with_dst(RootSrc<I8>{ ChanSrc<I8>{ w.chan, w.N }, rowp, w.right ? 1u : 0u });
-        else if (s < w.ly.Sl)
-            with_dst(LdsSrc{ w.lds_stage(s), sl });
-        else
-            with_dst(GlbSrc{ w.glb_stage(s), sl });
-    } else if (act) { // h = 1..8: stage s is 2h bytes of one unit
-        w.with_src(s, [&](const auto& src) {
-            w.with_dst(cs, [&](const auto& dst) {
-                const uint4 d = src.ld(0);
-                const uint32_t nib = g ? w.bits_at(o, h) : 0u;
-                uint32_t v[2] = { 0u, 0u };
-                for (uint32_t k = 0; k < h; ++k) {
-                    const int l = byte_of(d, k), r = byte_of(d, k + h);
-                    const uint32_t q = ubyte(g ? fip_g(l, r, (nib >> k) & 1u) : fip_f(l, r), k & 3u);
-                    if (k < 4)
-                        v[0] |= q;
-                    else
-                        v[1] |= q;
-                }
-                dst.st(0, make_uint4(v[0], v[1], 0u, 0u));
-            });
-        });
-    }
-    w.own(cs);
-}
+// F / G of the node at stage s (n = 2^s) into stage s-1 of the own lane
 template <int LP, bool I8>
 PCG_DEV void op_fg(Wave<LP, I8>& w, bool g, uint32_t s, uint32_t o, bool act)
 {
+    const uint32_t cs = s - 1, h = 1u << cs;
     if (s == w.top) { // the root's children are recomputed, never stored
         w.right = g;
         return;
     }
-    const uint32_t hq = s >= 5u ? 1u << (s - 5u) : 1u;
-    op_fg_at(w, g, s, o, act, w.slot(s), w.lane, w.row(), 0u, hq);
+    if (act) {
+        w.with_src(s, [&](const auto& src) {
+            w.with_dst(cs, [&](const auto& dst) {
+                if (h >= 16) {
+                    const uint32_t hq = h >> 4;
+                    uint32_t c = 0;
+                    for (; c + 2 <= hq; c += 2) { // two units in flight
+                        const uint4 a0 = src.ld(c), b0 = src.ld(c + hq), a1 = src.ld(c + 1), b1 = src.ld(c + 1 + hq);
+                        if (g) {
+                            const uint32_t bb = w.bits_at(o + 16u * c, 32);
+                            dst.st(c, g16(a0, b0, bb & 0xffffu));
+                            dst.st(c + 1, g16(a1, b1, bb >> 16));
+                        } else {
+                            dst.st(c, f16(a0, b0));
+                            dst.st(c + 1, f16(a1, b1));
+                        }
+                    }
+                    if (c < hq) { // hq == 1
+                        const uint4 a = src.ld(c), b = src.ld(c + hq);
+                        dst.st(c, g ? g16(a, b, w.bits_at(o + 16u * c, 16)) : f16(a, b));
+                    }
+                } else { // h = 1..8: stage s is 2h bytes of one unit
+                    const uint4 d = src.ld(0);
+                    const uint32_t nib = g ? w.bits_at(o, h) : 0u;
+                    uint32_t v[2] = { 0u, 0u };
+                    for (uint32_t k = 0; k < h; ++k) {
+                        const int l = byte_of(d, k), r = byte_of(d, k + h);
+                        const uint32_t q = ubyte(g ? fip_g(l, r, (nib >> k) & 1u) : fip_f(l, r), k & 3u);
+                        if (k < 4)
+                            v[0] |= q;
+                        else
+                            v[1] |= q;
+                    }
+                    dst.st(0, make_uint4(v[0], v[1], 0u, 0u));
+                }
+            });
+        });
+    }
+    w.own(cs);
 }
 
 // ---- F / G with more lanes than paths (round 6) ------------------------------------------
@@ -248,7 +224,7 @@ PCG_DEV void op_fg(Wave<LP, I8>& w, bool g, uint32_t s, uint32_t o, bool act)
 template <int LP, bool I8>
 PCG_DEV void op_fg_shared(Wave<LP, I8>& w, bool g, uint32_t s, uint32_t o, uint32_t P)
 {
-    const uint32_t hq = 1u << (s - 5); // output units (s >= 6: h = 2^(s-1) >= 32 bytes)
+    const uint32_t cs = s - 1, hq = 1u << (cs - 4); // output units (h = 2^cs >= 32 bytes)
     uint32_t pp = 1;
     while (pp < P)
         pp <<= 1;
@@ -257,9 +233,39 @@ PCG_DEV void op_fg_shared(Wave<LP, I8>& w, bool g, uint32_t s, uint32_t o, uint3
         hs >>= 1;
     const uint32_t path = w.p & (pp - 1), i = w.p / pp, dl = w.gb | path;
     const uint64_t pptr = __shfl(w.ptr, (int)dl, 64);
-    const uint32_t sl = w.gb | (uint32_t)((pptr >> (5u * s)) & 31u);
-    const uint32_t n = hq / hs; // this lane's units [n i, n i + n)
-    op_fg_at(w, g, s, o, path < P && i < hs, sl, dl, w.lds + w.ly.bits + dl, n * i, n);
+    const uint32_t* prow = w.lds + w.ly.bits + dl;   // the path's bit row, word q at [q * 64]
+    const uint32_t n = hq / hs, c0 = n * i;          // this lane's units [c0, c0 + n)
+    const bool act = path < P && i < hs;
+    if (act) {
+        const uint32_t sl = w.gb | (uint32_t)((pptr >> (5u * s)) & 31u);
+        auto run = [&](const auto& src, const auto& dst) {
+#pragma unroll 1
+            for (uint32_t c = c0; c < c0 + n; c += 2) { // (n even: hq >= 2 hs)
+                const uint4 a0 = src.ld(c), b0 = src.ld(c + hq), a1 = src.ld(c + 1), b1 = src.ld(c + 1 + hq);
+                if (g) {
+                    const uint32_t p0 = o + 16u * c, bb = prow[(p0 >> 5) << 6] >> (p0 & 31u);
+                    dst.st(c, g16(a0, b0, bb & 0xffffu));
+                    dst.st(c + 1, g16(a1, b1, bb >> 16));
+                } else {
+                    dst.st(c, f16(a0, b0));
+                    dst.st(c + 1, f16(a1, b1));
+                }
+            }
+        };
+        auto with_dst = [&](const auto& src) {
+            if (cs < w.ly.Sl)
+                run(src, LdsDst{ w.lds_stage(cs), dl });
+            else
+                run(src, GlbDst{ w.glb_stage(cs), dl });
+        };
+        if (s == w.ly.mt)
+            with_dst(RootSrc<I8>{ ChanSrc<I8>{ w.chan, w.N }, prow, w.right ? 1u : 0u });
+        else if (s < w.ly.Sl)
+            with_dst(LdsSrc{ w.lds_stage(s), sl });
+        else
+            with_dst(GlbSrc{ w.glb_stage(s), sl });
+    }
+    w.own(cs);
 }
 
 // The left child of the root (stage top-1, F(y_j, y_j+N/2): the same bytes for every path) read
@@ -268,24 +274,26 @@ PCG_DEV void op_fg_shared(Wave<LP, I8>& w, bool g, uint32_t s, uint32_t o, uint3
 // path reads the two units of an output from their lane (ds_bpermute), instead of every path
 // recomputing all of them (two channel loads and an F per unit).
 template <int LP, bool I8, int SLOTS>
-PCG_DEV void op_fg_rootl_slots(Wave<LP, I8>& w, bool g, uint32_t o, bool act)
+PCG_DEV void op_fg_rootl_slots(Wave<LP, I8>& w, bool g, uint32_t o, uint32_t hq, bool act)
 {
-    // unit u of the child (2 hq = 2 SLOTS LP units) is computed by lane u mod LP; pass k needs the
-    // units k LP + q (an output's a) and (k + SLOTS) LP + q (its b), q < LP: two units per lane live
+    // unit u of the child (2 hq = 2 SLOTS LP units) is computed by lane u mod LP as its u[u / LP]
     const RootSrc<I8> rs{ ChanSrc<I8>{ w.chan, w.N }, w.row(), 0u };
+    uint4 u[2 * SLOTS];
+#pragma unroll
+    for (int k = 0; k < 2 * SLOTS; ++k)
+        u[k] = rs.ld((uint32_t)k * LP + w.p);
     const uint32_t cs = w.ly.mt - 1;
     auto run = [&](const auto& dst) {
 #pragma unroll
         for (int k = 0; k < SLOTS; ++k) {
-            const uint4 ua = rs.ld((uint32_t)k * LP + w.p), ub = rs.ld((uint32_t)(k + SLOTS) * LP + w.p);
-#pragma unroll 1
+#pragma unroll 1 // (one output unit at a time: the kernel stays at 4 waves per SIMD)
             for (uint32_t q = 0; q < (uint32_t)LP; ++q) {
                 const int sl = (int)(w.gb | q);
                 const uint32_t c = (uint32_t)k * LP + q; // output unit: a = unit c, b = unit c + hq
-                const uint4 a = make_uint4(__shfl(ua.x, sl, 64), __shfl(ua.y, sl, 64), __shfl(ua.z, sl, 64),
-                                           __shfl(ua.w, sl, 64));
-                const uint4 b = make_uint4(__shfl(ub.x, sl, 64), __shfl(ub.y, sl, 64), __shfl(ub.z, sl, 64),
-                                           __shfl(ub.w, sl, 64));
+                const uint4 a = make_uint4(__shfl(u[k].x, sl, 64), __shfl(u[k].y, sl, 64), __shfl(u[k].z, sl, 64),
+                                           __shfl(u[k].w, sl, 64));
+                const uint4 b = make_uint4(__shfl(u[k + SLOTS].x, sl, 64), __shfl(u[k + SLOTS].y, sl, 64),
+                                           __shfl(u[k + SLOTS].z, sl, 64), __shfl(u[k + SLOTS].w, sl, 64));
                 if (!act)
                     continue;
                 if (g)
@@ -299,6 +307,7 @@ PCG_DEV void op_fg_rootl_slots(Wave<LP, I8>& w, bool g, uint32_t o, bool act)
         run(LdsDst{ w.lds_stage(cs), w.lane });
     else
         run(GlbDst{ w.glb_stage(cs), w.lane });
+    (void)hq;
 }
 template <int LP, bool I8>
 PCG_DEV bool op_fg_rootl(Wave<LP, I8>& w, bool g, uint32_t s, uint32_t o, bool act)
@@ -309,9 +318,9 @@ PCG_DEV bool op_fg_rootl(Wave<LP, I8>& w, bool g, uint32_t s, uint32_t o, bool a
     if (hq < (uint32_t)LP || 2u * hq > 4u * LP)
         return false;
     if (hq == (uint32_t)LP)
-        op_fg_rootl_slots<LP, I8, 1>(w, g, o, act);
+        op_fg_rootl_slots<LP, I8, 1>(w, g, o, hq, act);
     else
-        op_fg_rootl_slots<LP, I8, 2>(w, g, o, act);
+        op_fg_rootl_slots<LP, I8, 2>(w, g, o, hq, act);
     w.own(s - 1);
     return true;
 }

@@ -31,6 +31,8 @@ def main():
         r = d["roofline"]
         fpl, bpc, peak = r["frames_per_launch"], r["algorithmic_bytes_per_codeword"], r["peak"]
         frac_trace = fpl * bpc / (avg * 1e-3) / 1e9 / peak
+        if r.get("kernel_ms_scope"):  # adaptive modes: the events bracket more than this kernel
+            print(f"  ({tag}: kernel_ms is {r['kernel_ms_scope']} -- not this kernel's own time)")
         print(f"  {tag:12s} kernel_ms {r['kernel_ms']:.4f} (trace/events {avg / r['kernel_ms']:.3f}), "
               f"ms_per_step {d['ms_per_step']:.4f}, frac {r['frac']:.5f} vs {frac_trace:.5f} from the trace "
               f"({100 * (frac_trace / r['frac'] - 1):+.1f} %)")
