@@ -1198,22 +1198,26 @@ static void par_memcpy(void* dst, const void* src, size_t bytes, int threads, bo
 // piece: the host threads (started once) each copy their share of piece k and count it done; the
 // calling thread issues piece k's DMA as soon as every share has landed, while the threads go on
 // with piece k+1.
-static hipError_t staged_copy(void* h, void* d, const char* src, size_t bytes, size_t piece, int threads, bool nt,
-                              hipStream_t st)
+static hipError_t staged_copy(void* h, void* d, const char* src, size_t bytes, size_t piece0, size_t piece,
+                              int threads, bool nt, hipStream_t st)
 {
     if (piece >= bytes || threads <= 1) {
         par_memcpy(h, src, bytes, threads, nt);
         return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st);
     }
+    // piece i = [off(i), off(i + 1)): the first one piece0 long (the copy engine starts sooner),
+    // then piece
+    piece0 = std::min(piece0, piece);
+    auto off = [&](size_t i) { return i == 0 ? size_t(0) : std::min(bytes, piece0 + (i - 1) * piece); };
+    const size_t np = 1 + (bytes > piece0 ? (bytes - piece0 + piece - 1) / piece : 0);
     auto cp = nt ? nt_memcpy : [](void* dd, const void* ss, size_t n) { memcpy(dd, ss, n); };
-    const size_t np = (bytes + piece - 1) / piece;
     std::vector<std::atomic<int>> done(np);
     for (auto& x : done)
         x.store(0, std::memory_order_relaxed);
     const int t = threads;
     auto work = [&](int k) {
         for (size_t i = 0; i < np; ++i) {
-            const size_t o = i * piece, pb = std::min(piece, bytes - o);
+            const size_t o = off(i), pb = off(i + 1) - o;
             const size_t part = ((pb + t - 1) / t + 4095) & ~size_t(4095), a = part * (size_t)k;
             if (a < pb)
                 cp((char*)h + o + a, src + o + a, std::min(part, pb - a));
@@ -1227,8 +1231,8 @@ static hipError_t staged_copy(void* h, void* d, const char* src, size_t bytes, s
     for (size_t i = 0; i < np && e == hipSuccess; ++i) {
         while (done[i].load(std::memory_order_acquire) < t)
             std::this_thread::yield();
-        const size_t o = i * piece;
-        e = hipMemcpyAsync((char*)d + o, (const char*)h + o, std::min(piece, bytes - o), hipMemcpyHostToDevice, st);
+        const size_t o = off(i);
+        e = hipMemcpyAsync((char*)d + o, (const char*)h + o, off(i + 1) - o, hipMemcpyHostToDevice, st);
     }
     for (auto& x : th)
         x.join();
@@ -1344,6 +1348,8 @@ static int decode_host(pcg_plan* p, const void* llr, size_t elem, uint64_t F, ui
     // caller buffer, no staging: 1.127e7)
     const int piece_mb = env_int("PCG_HOST_PIECE_MB", 16);
     const size_t piece = piece_mb > 0 ? (size_t)piece_mb << 20 : ~size_t(0);
+    // the batch's first piece is shorter (PCG_HOST_FIRST_KB, default 2048): nothing overlaps its staging
+    const size_t piece_first = (size_t)std::max(env_int("PCG_HOST_FIRST_KB", 2048), 64) << 10;
     int rc = pipe_alloc(p, chunk, fb, stage);
     if (rc != 0)
         return rc;
@@ -1434,7 +1440,8 @@ static int decode_host(pcg_plan* p, const void* llr, size_t elem, uint64_t F, ui
             // staged in pieces, each copied as soon as it is staged: the DMA of piece k overlaps
             // the staging of piece k+1, so the copy engine starts after one piece (not one whole
             // chunk) and the pipeline's fill is a piece long
-            if ((e = staged_copy(q->h_in[b], q->d_in[b], src, nb, piece, threads, nt, q->copy)) != hipSuccess)
+            if ((e = staged_copy(q->h_in[b], q->d_in[b], src, nb, i == 0 ? piece_first : piece, piece, threads, nt,
+                                 q->copy)) != hipSuccess)
                 return hip_fail(e, "hipMemcpyAsync(H2D)");
         } else if (!done) {
             if ((e = hipMemcpyAsync(q->d_in[b], src, nb, hipMemcpyHostToDevice, q->copy)) != hipSuccess)

@@ -68,11 +68,14 @@ print(f"serial (PCG_HOST_PIPE=0) {rate(llr, PCG_HOST_PIPE=0):.4g} cw/s")
 if "pieces" in sys.argv[1:]:
     for chunk in (16384, 32768):
         print(f"page-locked caller buffer, chunk {chunk}: {rate(pinned.numpy(), PCG_HOST_CHUNK=chunk):.4g} cw/s")
-    for thr in (8, 12, 16):
-        for chunk in (16384, 32768):
-            for pmb in (0, 2, 4, 8, 16):
-                r = rate(llr, PCG_HOST_PIPE=2, PCG_HOST_THREADS=thr, PCG_HOST_CHUNK=chunk, PCG_HOST_PIECE_MB=pmb)
-                print(f"pinned staging (2), {thr} threads, chunk {chunk}, piece {pmb} MB: {r:.4g} cw/s", flush=True)
+    for thr in (8, 12):
+        for chunk in (8192, 16384):
+            for pmb in (0, 8, 16):
+                for fkb in ((16384, 2048, 256) if pmb else (2048,)):
+                    r = rate(llr, PCG_HOST_PIPE=2, PCG_HOST_THREADS=thr, PCG_HOST_CHUNK=chunk, PCG_HOST_PIECE_MB=pmb,
+                             PCG_HOST_FIRST_KB=fkb)
+                    print(f"pinned staging (2), {thr} threads, chunk {chunk}, piece {pmb} MB, first piece {fkb} KB: "
+                          f"{r:.4g} cw/s", flush=True)
     sys.exit(0)
 for chunk in (16384, 32768):
     print(f"pageable runtime copies (1), chunk {chunk}: {rate(llr, PCG_HOST_PIPE=1, PCG_HOST_CHUNK=chunk):.4g} cw/s")
