@@ -97,7 +97,7 @@ def random_list_codes():
     # staged ops, with a fused / unfused child and both recomputed levels (own stream: the entries
     # above keep their frozen sets and cache files)
     g = _xorshift(0x5C1A12)
-    for N, L in ((512, 8), (1024, 8), (1024, 4)):
+    for N, L in ((512, 8), (1024, 8), (1024, 4), (64, 2), (256, 5), (512, 16), (1024, 32), (2048, 8), (1024, 12)):
         nf = N // 4 + next(g) % (N // 2)
         pos = list(range(N))
         for i in range(N - 1, 0, -1):
