@@ -221,6 +221,10 @@ PCG_DEV void op_fg(Wave<LP, I8>& w, bool g, uint32_t s, uint32_t o, bool act)
 #ifndef PCG_SCLC_MINW
 #define PCG_SCLC_MINW 4
 #endif
+// list pruning on keys in registers instead of the group's LDS candidate array (0: the LDS version)
+#ifndef PCG_SCLC_RPRUNE
+#define PCG_SCLC_RPRUNE 1 // measured: scl8_char 2.93e7 -> 2.99e7 cw/s (profiles/r06k_scl8_char_register_pruning_ab.txt)
+#endif
 template <int LP, bool I8>
 PCG_DEV void op_fg_shared(Wave<LP, I8>& w, bool g, uint32_t s, uint32_t o, uint32_t P)
 {
@@ -488,8 +492,10 @@ PCG_DEV void op_branch(Wave<LP, I8>& w, uint32_t kind, uint32_t s, uint32_t o, u
     // candidate keys metric << 8 | index (|metric| < 2^23 for N <= 32768, index < 256)
     // group stride 9 LP: the 64/LP groups' lanes hit distinct LDS banks in the pruning scans
     int* KV = reinterpret_cast<int*>(w.lds + w.ly.cand) + (w.gb / LP) * (9 * LP);
+    (void)KV;
     int T[4] = { 0, 0, 0, 0 };
     uint32_t I[4] = { 0, 0, 0, 0 }, par = 0;
+    int kvr[8] = { 0, 0, 0, 0, 0, 0, 0, 0 }; // PCG_SCLC_RPRUNE: the keys of positions p k + j in registers
     if (act) {
         int c[8];
         const int m = w.m;
@@ -544,8 +550,15 @@ PCG_DEV void op_branch(Wave<LP, I8>& w, uint32_t kind, uint32_t s, uint32_t o, u
             c[6] = mm - T[2] - T[3];
             c[7] = mm - wk - T[1] - T[2] - T[3];
         }
+#if PCG_SCLC_RPRUNE
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j)
+            if (j < k)
+                kvr[j] = (int)(((uint32_t)c[j] << 8) | (w.p * k + j));
+#else
         for (uint32_t j = 0; j < k; ++j)
             KV[w.p * k + j] = (int)(((uint32_t)c[j] << 8) | (w.p * k + j));
+#endif
     }
     wsync();
     SC_ADD(w.prof, 17 + kind, tb0);
@@ -553,6 +566,56 @@ PCG_DEV void op_branch(Wave<LP, I8>& w, uint32_t kind, uint32_t s, uint32_t o, u
     // simplePartialSortDescending(idx, metrics, np, size) (arrayfuncs.h:161-183)
     const uint32_t size = k * P, np = size < w.L ? size : w.L;
     const uint32_t lim = size - 1 < np ? size - 1 : np;
+#if PCG_SCLC_RPRUNE
+    // The same passes on the keys in registers: position q = p k + j is lane p's kvr[j].  Pass i
+    // takes the group's (max metric, lowest position) among positions >= i and swaps that
+    // position with position i -- a register select and two shuffles instead of LDS scans and
+    // a barrier per pass.
+    for (uint32_t i = 0; i < lim; ++i) {
+        int bv = INT_NEG;
+        uint32_t bq = 0xffffffffu;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t q = w.p * k + j;
+            if (j < k && q >= i && q < size) {
+                const int v = kvr[j] >> 8;
+                if (bq == 0xffffffffu || v > bv) {
+                    bv = v;
+                    bq = q;
+                }
+            }
+        }
+        grp_argmax_i<LP>(bv, bq);
+        const uint32_t ri = i & (k - 1u), rb = bq & (k - 1u), li = i >> lk, lb = bq >> lk;
+        int mi = kvr[0], mb = kvr[0];
+#pragma unroll
+        for (uint32_t j = 1; j < 8; ++j) {
+            mi = j == ri ? kvr[j] : mi;
+            mb = j == rb ? kvr[j] : mb;
+        }
+        const int ki = __shfl(mi, (int)(w.gb | li), 64), kb = __shfl(mb, (int)(w.gb | lb), 64);
+        if (bq != i) {
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j) {
+                if (w.p == li && j == ri)
+                    kvr[j] = kb;
+                if (w.p == lb && j == rb)
+                    kvr[j] = ki;
+            }
+        }
+    }
+    SC_ADD(w.prof, 20, tb1);
+    SC_T0(tb2);
+    // survivors: survivor q < np takes the key at position q (lane q / k, register q mod k)
+    const bool surv = w.p < np;
+    int key = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        const int x = __shfl(kvr[j], (int)(w.gb | (w.p >> lk)), 64);
+        key = j == (w.p & (k - 1u)) ? x : key;
+    }
+    key = surv ? key : 0;
+#else
     for (uint32_t i = 0; i < lim; ++i) {
         int bv = INT_NEG;
         uint32_t bq = 0xffffffffu;
@@ -576,6 +639,7 @@ PCG_DEV void op_branch(Wave<LP, I8>& w, uint32_t kind, uint32_t s, uint32_t o, u
     // survivors
     const bool surv = w.p < np;
     const int key = surv ? KV[w.p] : 0;
+#endif
     const uint32_t id = (uint32_t)key & 0xffu;
     const int nm = key >> 8;
     wsync();
