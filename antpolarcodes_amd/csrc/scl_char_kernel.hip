@@ -43,6 +43,13 @@ namespace {
 
 constexpr int INT_NEG = -2147483647 - 1;
 
+// list pruning on keys in registers instead of the group's LDS candidate array (0: the LDS version,
+// whose candidate region the layout then reserves: host part and kernel must be built alike, i.e. set
+// it in a dev library build, not through PCG_RTC_XOPTS alone -- sclc_body refuses a mismatch)
+#ifndef PCG_SCLC_RPRUNE
+#define PCG_SCLC_RPRUNE 1 // measured: scl8_char 2.93e7 -> 2.99e7 cw/s (profiles/r06k_scl8_char_register_pruning_ab.txt)
+#endif
+
 // dev-only per-phase cycle profile (build with -DPCG_SCLC_PROF, run with PCG_OPPROF=1;
 // tools/sclc_prof.py): buckets 1 F, 2 G, 4 COMB, 16 R0, 17 R1, 18 Rep, 19 SPC
 // (candidates), 20 pruning, 21 survivors, 22 final extraction, 61 total, 62 groups
@@ -81,7 +88,7 @@ __host__ __device__ inline Layout make_layout(uint32_t N, uint32_t Sl)
     y.bits = 256u * st_units(y.Sl);
     const uint32_t W = N >= 32 ? N / 32 : 1u;
     y.cand = y.bits + 64u * W;
-    y.lds = y.cand + 576u;
+    y.lds = y.cand + (PCG_SCLC_RPRUNE ? 0u : 576u); // (the register pruning needs no candidate region)
     y.gdwords = 256ull * (st_units(y.mt) - st_units(y.Sl));
     return y;
 }
@@ -216,14 +223,10 @@ PCG_DEV void op_fg(Wave<LP, I8>& w, bool g, uint32_t s, uint32_t o, bool act)
 #ifndef PCG_SCLC_ROOTL
 #define PCG_SCLC_ROOTL 1
 #endif
-// waves per SIMD the register allocation must allow (<= 128 VGPRs: the 14 waves per CU that the
-// 12 KB LDS budget gives)
+// waves per SIMD the register allocation must allow (<= 128 VGPRs: the 16 waves per CU that the
+// 10 KB LDS budget allows)
 #ifndef PCG_SCLC_MINW
 #define PCG_SCLC_MINW 4
-#endif
-// list pruning on keys in registers instead of the group's LDS candidate array (0: the LDS version)
-#ifndef PCG_SCLC_RPRUNE
-#define PCG_SCLC_RPRUNE 1 // measured: scl8_char 2.93e7 -> 2.99e7 cw/s (profiles/r06k_scl8_char_register_pruning_ab.txt)
 #endif
 template <int LP, bool I8>
 PCG_DEV void op_fg_shared(Wave<LP, I8>& w, bool g, uint32_t s, uint32_t o, uint32_t P)
@@ -718,6 +721,8 @@ PCG_DEV void sclc_body(const KernelArgs& a, uint32_t Sl)
     w.top = a.log2N;
     w.L = a.L;
     w.ly = make_layout(a.N, Sl);
+    if (w.ly.lds > a.wave_lds_floats) // a kernel built unlike the host part that sized its LDS: refuse
+        return;
     w.gs = reinterpret_cast<uint32_t*>(a.scratch) + (uint64_t)blockIdx.x * w.ly.gdwords;
     w.lane = threadIdx.x & 63;
     w.prof = a.prof;
@@ -914,13 +919,16 @@ uint32_t lp_of(uint32_t L)
 } // namespace
 
 // LDS / scratch layout: stages < Sl in LDS, chosen so a wave's LDS stays within
-// PCG_SCLC_LDS_KB (default 12 KB: only the shared small-stage unit in LDS at N = 1024, 14
-// waves per CU -- occupancy beats LDS residency here, measured at N = 1024, L = 8).
+// PCG_SCLC_LDS_KB (default 10 KB: the bit rows and stages < 5 at N = 1024 -- 16 waves per CU, the
+// 4-waves-per-SIMD register limit; occupancy beats LDS residency here.  Measured at N = 1024,
+// L = 8 once the pruning moved to registers and its 2.3 KB candidate region went away,
+// profiles/r06n_scl8_char_lds_budget_sweep.txt: 12 KB (stages < 6, 13 waves / CU) 2.21e7 cw/s,
+// 10 KB 3.16-3.19e7, 9 KB (stages < 4) 3.16e7; round 5's 12 KB with the candidate region: 2.99e7).
 int sclc_layout(uint32_t N, uint32_t L, uint32_t* lds_dwords, uint32_t* Sl, uint64_t* scratch_dwords)
 {
     if (L < 2 || L > 32 || N < 8)
         return -4;
-    uint32_t budget = 12u * 1024u;
+    uint32_t budget = (PCG_SCLC_RPRUNE ? 10u : 12u) * 1024u;
     if (const char* e = getenv("PCG_SCLC_LDS_KB"))
         budget = (uint32_t)atoi(e) * 1024u;
     const uint32_t top = (uint32_t)__builtin_ctz(N);

@@ -198,7 +198,7 @@ def test_sclc_layout_variants(oracle, monkeypatch):
     rng = np.random.default_rng(9)
     fr = frozen_bits(1024, 512, 0.0)
     x8 = i8_kinds(rng, 64, 1024, "normal")
-    for kb in ("12", "20", "40", "80"):
+    for kb in ("9", "10", "12", "20", "40", "80"):
         monkeypatch.setenv("PCG_SCLC_LDS_KB", kb)
         _check(oracle, 1024, 8, fr, x8)
 
