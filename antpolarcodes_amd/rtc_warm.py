@@ -92,8 +92,13 @@ def warm(jobs=None, quiet=False, strict=True, cache=None, todo=None):
     cache = cache or CACHE
     os.makedirs(cache, exist_ok=True)
     todo = codes() if todo is None else todo
-    ver = hiprtc_version()
-    if dir_version(cache) != ver:
+    try:
+        ver = hiprtc_version()
+    except (subprocess.CalledProcessError, IndexError, OSError) as e:  # (the library does not load here)
+        ver = None
+        print(f"WARNING: rtc cache: hiprtc version unknown ({e}); {cache}/HIPRTC_VERSION left as it is",
+              file=sys.stderr)
+    if ver and ver != "none" and dir_version(cache) != ver:
         with open(os.path.join(cache, "HIPRTC_VERSION"), "w") as f:
             f.write(ver + "\n")
     jobs = jobs or min(8, os.cpu_count() or 1)
